@@ -1,0 +1,826 @@
+// rt_render.hip — gfx950 kernels and pass orchestration of the MI355X path tracer.
+//
+// Replaces gpu_raytrace (reference raytracing.cu:170-284) and the per-ray device functions it
+// launches (scene.cu:78-487), plus the bloom kernels (raytracing.cu:21-74).  Design:
+//   * one lane per ray slot, 256-thread workgroups (4 wave64s);
+//   * BVH as 64-B "child-pair" records: an internal node stores both children's AABBs and
+//     their refs, so one 64-B load feeds both slab tests (the reference reads 32 B for the
+//     popped node plus 2 x 32 B for the children); leaves are encoded in the ref itself;
+//   * per-lane traversal stack in LDS, [entry][lane] layout (conflict-free ds_*_b64), with
+//     a private overflow tail; the top-of-stack child is kept in registers, so only the
+//     deferred (near) child of a two-hit node is ever pushed.  Pop order is the reference's
+//     (far child first, scene.cu:204-225), so hits and tie-breaks are identical;
+//   * the ray reorder is a stable 65-bucket multisplit (6 live key bits + terminated,
+//     SURVEY §8a rows K/L): tile histograms, per-bucket scan, and a scatter that ranks with
+//     seven 64-lane __ballot()s per round;
+//   * accumulation is an ordered per-pixel sum (deterministic; no float atomics).
+#include "rt_abi.h"
+#include "rt_device.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+namespace rtamd {
+int fail(int code, const std::string &msg);
+}
+
+using namespace rtd;
+
+namespace {
+
+constexpr int kBlock = 256;           // threads per workgroup (4 waves)
+constexpr int kStackLds = 16;         // stack entries per lane kept in LDS
+constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138)
+constexpr int kSortItems = 16;        // sort tile = kBlock * kSortItems slots
+constexpr int kSortTile = kBlock * kSortItems;
+constexpr int kBuckets = 65;
+constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFFFFF)
+constexpr uint32_t kLeaf = 0x80000000u, kBigLeaf = 0x40000000u;
+
+struct DevScene {
+    const float4 *spheres;            // center.xyz, radius
+    const float4 *tris;               // 3 x float4: p1.xyz e1.x | e1.yz e2.xy | e2.z n.xyz
+    const uint16_t *mat_idx;
+    const float4 *mats;               // 3 x float4: diffuse,metal | specular,rough | emit,ior
+    const float4 *nodes;              // 4 x float4 per internal node (child-pair record)
+    const int2 *big_leaves;           // {begin, end} for leaves that do not fit a ref
+    const float *env;                 // env_h * env_w * 3
+    int sphere_count, env_w, env_h, width, height;
+    uint32_t root_ref;
+    V3 cam, tl, sr, su, min_coord, inv_dim;
+    float inv_w, inv_h;
+};
+
+struct Counters {                     // device-side work counters (u64, one atomic per wave)
+    unsigned long long live, pn, iv, tt, st, hits, misses, pad;
+};
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
+    unsigned long long s = v;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    return s;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// ---------------------------------------------------------------- ray generation
+// scene.cu:78-105 + raytracing.cu:76-81.  Ray layout: 3 x float4 = origin, dir, T, C.
+__global__ __launch_bounds__(kBlock) void generate_kernel(DevScene S, float4 *__restrict__ rays,
+                                                          uint32_t *__restrict__ idx, uint8_t *__restrict__ bkt,
+                                                          int rtc, int n, uint32_t seed_term) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    Rng rng = pcg_seed((uint32_t)i * 0x85810BEAu + seed_term);   // 298592570346 mod 2^32
+    const int pixel = i / rtc;
+    const int x = pixel % S.width, y = pixel / S.width;
+    idx[i] = (uint32_t)i;
+    bkt[i] = 0;
+    const float xc = (x + random01(rng)) * S.inv_w;
+    const float yc = (y + random01(rng)) * S.inv_h;
+    const V3 d = normalise(S.tl + xc * S.sr - yc * S.su);
+    float4 *r = rays + (size_t)i * 3;
+    r[0] = make_float4(S.cam.x, S.cam.y, S.cam.z, d.x);
+    r[1] = make_float4(d.y, d.z, 1.0f, 1.0f);
+    r[2] = make_float4(1.0f, 0.0f, 0.0f, 0.0f);
+}
+
+// ---------------------------------------------------------------- traversal
+template <bool COUNT>
+struct Work { unsigned pn = 0, iv = 0, tt = 0; };
+
+// bvh_closest_hit_distance, scene.cu:134-241.  `col` = this lane's LDS stack column.
+template <bool COUNT>
+__device__ __forceinline__ void traverse(const DevScene &S, V3 o, V3 d, float &closest, int &index, uint2 *col,
+                                         Work<COUNT> &w) {
+    const float ix = 1 / d.x, iy = 1 / d.y, iz = 1 / d.z;
+    uint2 ovf[kStackMax - kStackLds];
+    uint32_t ref = S.root_ref;      // root is popped with distance 0 < closest
+    int sp = 0;
+    while (true) {
+        if (COUNT) w.pn++;
+        bool descend = false;
+        if (!(ref & kLeaf)) {
+            if (COUNT) w.iv++;
+            const float4 *nd = S.nodes + (size_t)ref * 4;
+            const float4 a = nd[0], b = nd[1], c = nd[2];
+            const uint4 kids = *reinterpret_cast<const uint4 *>(nd + 3);
+            float t0, t1;
+            const bool h0 = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, ix, iy, iz, closest, t0);
+            const bool h1 = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, ix, iy, iz, closest, t1);
+            if (h0 && h1) {
+                // Reference pushes near then far; the far child is popped next.
+                uint2 below;
+                float ttop;
+                if (t0 < t1) { below = make_uint2(kids.x, __float_as_uint(t0)); ref = kids.y; ttop = t1; }
+                else { below = make_uint2(kids.y, __float_as_uint(t1)); ref = kids.x; ttop = t0; }
+                if (sp < kStackLds) col[sp * kBlock] = below; else ovf[sp - kStackLds] = below;
+                sp++;
+                descend = !(ttop >= closest);
+            } else if (h0) {
+                ref = kids.x;
+                descend = !(t0 >= closest);
+            } else if (h1) {
+                ref = kids.y;
+                descend = !(t1 >= closest);
+            }
+        } else {
+            int begin, end;
+            if (ref & kBigLeaf) {
+                const int2 be = S.big_leaves[ref & 0x3FFFFFFFu];
+                begin = be.x; end = be.y;
+            } else {
+                begin = (int)(ref & 0xFFFFFFu);
+                end = begin + (int)((ref >> 24) & 0x3Fu);
+            }
+            for (int i = begin; i < end; i++) {       // Möller–Trumbore, scene.cu:160-195
+                if (COUNT) w.tt++;
+                const float4 *tp = S.tris + (size_t)i * 3;
+                const float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
+                const V3 p1 = v3(q0.x, q0.y, q0.z), e1 = v3(q0.w, q1.x, q1.y), e2 = v3(q1.z, q1.w, q2.x);
+                float t;
+                if (!ray_triangle(o, d, p1, e1, e2, closest, t)) continue;
+                closest = t;
+                index = S.sphere_count + i;
+            }
+        }
+        if (descend) continue;
+        bool found = false;
+        while (sp > 0) {
+            sp--;
+            const uint2 e = sp < kStackLds ? col[sp * kBlock] : ovf[sp - kStackLds];
+            if (!(__uint_as_float(e.y) >= closest)) { ref = e.x; found = true; break; }
+        }
+        if (!found) break;
+    }
+}
+
+// One bounce for one slot: raytracing.cu:83-94 -> Scene::process_ray (scene.cu:320-487).
+template <bool SORTED, bool COUNT>
+__global__ __launch_bounds__(kBlock) void process_kernel(DevScene S, float4 *__restrict__ rays,
+                                                         const uint32_t *__restrict__ idx, uint8_t *__restrict__ bkt,
+                                                         int n, uint32_t seed_term, Counters *__restrict__ ctr) {
+    __shared__ uint2 stack[kStackLds * kBlock];
+    const int slot = blockIdx.x * kBlock + threadIdx.x;
+    const bool live = slot < n && bkt[slot] != kDead;
+    Work<COUNT> w;
+    unsigned hit = 0, miss = 0;
+    if (live) {
+        Rng rng = pcg_seed((uint32_t)slot * 4137874753u + seed_term);
+        const uint32_t ri = SORTED ? idx[slot] : (uint32_t)slot;
+        float4 *rp = rays + (size_t)ri * 3;
+        const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+        const V3 o = v3(r0.x, r0.y, r0.z), d = v3(r0.w, r1.x, r1.y);
+        V3 T = v3(r1.z, r1.w, r2.x), C = v3(r2.y, r2.z, r2.w);
+        float closest = 1e30f;
+        int index = -1;
+        for (int i = 0; i < S.sphere_count; i++) {   // scene.cu:338-372
+            const float4 sp = S.spheres[i];
+            float t;
+            if (ray_sphere(o, d, v3(sp.x, sp.y, sp.z), sp.w, closest, t)) { closest = t; index = i; }
+        }
+        traverse<COUNT>(S, o, d, closest, index, stack + threadIdx.x, w);
+        V3 no = o, nd = d;
+        if (index == -1) {                             // scene.cu:376-395
+            miss = 1;
+            C = C + sky_color(S.env, S.env_w, S.env_h, d) * T;
+            T = v3(0, 0, 0);
+        } else {
+            hit = 1;
+            no = o + closest * d;
+            V3 normal;
+            if (index < S.sphere_count) {
+                const float4 sp = S.spheres[index];
+                normal = (1 / sp.w) * (no - v3(sp.x, sp.y, sp.z));
+            } else {
+                const float4 q2 = S.tris[(size_t)(index - S.sphere_count) * 3 + 2];
+                normal = v3(q2.y, q2.z, q2.w);
+            }
+            scatter(d, normal, load_mat(S.mats + (size_t)S.mat_idx[index] * 3), rng, T, C, nd);
+        }
+        rp[0] = make_float4(no.x, no.y, no.z, nd.x);
+        rp[1] = make_float4(nd.y, nd.z, T.x, T.y);
+        rp[2] = make_float4(T.z, C.x, C.y, C.z);
+        bkt[slot] = (uint8_t)(is_black(T) ? kDead : bucket_of(no, nd, S.min_coord, S.inv_dim));
+    }
+    const unsigned long long nlive = __popcll(__ballot(live));
+    if (lane_id() == 0 && nlive) atomicAdd(&ctr->live, nlive);
+    if (COUNT) {
+        const unsigned long long a = wave_sum(w.pn), b = wave_sum(w.iv), c = wave_sum(w.tt);
+        const unsigned long long h = wave_sum(hit), m = wave_sum(miss);
+        if (lane_id() == 0 && nlive) {
+            atomicAdd(&ctr->pn, a);
+            atomicAdd(&ctr->iv, b);
+            atomicAdd(&ctr->tt, c);
+            atomicAdd(&ctr->hits, h);
+            atomicAdd(&ctr->misses, m);
+            atomicAdd(&ctr->st, nlive * (unsigned long long)S.sphere_count);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- stable 65-bucket reorder
+// Equivalent to cub::DeviceRadixSort::SortPairs on the reference keys (raytracing.cu:238-247).
+// Peers = lanes of the wave holding the same bucket, from seven 64-lane ballots.
+__device__ __forceinline__ unsigned long long match_bucket(uint32_t b, bool valid) {
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 7; bit++) {
+        const unsigned long long m = __ballot((b >> bit) & 1u);
+        peers &= ((b >> bit) & 1u) ? m : ~m;
+    }
+    return peers;
+}
+
+__device__ __forceinline__ uint32_t rank_below(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Per-tile bucket counts, written bucket-major: counts[b * tiles + tile].
+__global__ __launch_bounds__(kBlock) void sort_hist_kernel(const uint8_t *__restrict__ bkt, int n, int tiles,
+                                                           uint32_t *__restrict__ counts) {
+    __shared__ uint32_t h[kBuckets];
+    for (int b = threadIdx.x; b < kBuckets; b += kBlock) h[b] = 0;
+    __syncthreads();
+    const int base = blockIdx.x * kSortTile;
+#pragma unroll 4
+    for (int r = 0; r < kSortItems; r++) {
+        const int item = base + r * kBlock + threadIdx.x;
+        const bool valid = item < n;
+        const uint32_t b = valid ? bkt[item] : 0u;
+        const unsigned long long peers = match_bucket(b, valid);
+        if (valid && rank_below(peers) == 0) atomicAdd(&h[b], (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kBuckets; b += kBlock) counts[(size_t)b * tiles + blockIdx.x] = h[b];
+}
+
+// One workgroup per bucket: exclusive scan of that bucket's tile counts + bucket total.
+__global__ __launch_bounds__(kBlock) void sort_scan_kernel(const uint32_t *__restrict__ counts, int tiles,
+                                                           uint32_t *__restrict__ offsets, uint32_t *__restrict__ totals) {
+    __shared__ uint32_t wsum[kBlock / 64];
+    __shared__ uint32_t carry;
+    const int b = blockIdx.x;
+    const uint32_t *in = counts + (size_t)b * tiles;
+    uint32_t *out = offsets + (size_t)b * tiles;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int start = 0; start < tiles; start += kBlock) {
+        const int t = start + threadIdx.x;
+        const uint32_t v = t < tiles ? in[t] : 0u;
+        uint32_t x = v;                                  // inclusive wave scan
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t pre = carry;
+        for (int k = 0; k < wave; k++) pre += wsum[k];
+        if (t < tiles) out[t] = pre + x - v;
+        __syncthreads();
+        if (threadIdx.x == kBlock - 1) carry = pre + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) totals[b] = carry;
+}
+
+// Stable scatter: rounds of 256 consecutive slots; rank = earlier rounds + earlier waves +
+// earlier lanes holding the same bucket.
+__global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__restrict__ bkt_in,
+                                                              const uint32_t *__restrict__ idx_in, int n, int tiles,
+                                                              const uint32_t *__restrict__ offsets,
+                                                              const uint32_t *__restrict__ totals,
+                                                              uint8_t *__restrict__ bkt_out, uint32_t *__restrict__ idx_out) {
+    __shared__ uint32_t run[kBuckets];
+    __shared__ uint32_t wcount[kBlock / 64][kBuckets];
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int b = 0; b < kBuckets; b++) {
+            run[b] = acc + offsets[(size_t)b * tiles + blockIdx.x];
+            acc += totals[b];
+        }
+    }
+    for (int k = threadIdx.x; k < (kBlock / 64) * kBuckets; k += kBlock) (&wcount[0][0])[k] = 0;
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    const int base = blockIdx.x * kSortTile;
+    for (int r = 0; r < kSortItems; r++) {
+        const int item = base + r * kBlock + threadIdx.x;
+        const bool valid = item < n;
+        const uint32_t b = valid ? bkt_in[item] : 0u;
+        const uint32_t ix = valid ? idx_in[item] : 0u;
+        const unsigned long long peers = match_bucket(b, valid);
+        const uint32_t rank = rank_below(peers);
+        if (valid && rank == 0) wcount[wave][b] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = run[b] + rank;
+            for (int k = 0; k < wave; k++) pos += wcount[k][b];
+            idx_out[pos] = ix;
+            bkt_out[pos] = (uint8_t)b;
+        }
+        __syncthreads();
+        if (threadIdx.x < kBuckets) {
+            uint32_t s = 0;
+            for (int k = 0; k < kBlock / 64; k++) { s += wcount[k][threadIdx.x]; wcount[k][threadIdx.x] = 0; }
+            run[threadIdx.x] += s;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- accumulate
+// Ordered per-pixel sum of the pass's samples, then fb += sum (raytracing.cu:96-107 without
+// the unordered atomics; the CPU path's order, raytracing.cu:114-120).
+__global__ __launch_bounds__(kBlock) void accumulate_kernel(float *__restrict__ fb, const float4 *__restrict__ rays,
+                                                            int rtc, int pixels, float *__restrict__ pass_out) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= pixels) return;
+    float sx = 0, sy = 0, sz = 0;
+    const float4 *r = rays + (size_t)p * rtc * 3 + 2;
+    for (int s = 0; s < rtc; s++) {
+        const float4 c = r[(size_t)s * 3];
+        sx = sx + c.y;
+        sy = sy + c.z;
+        sz = sz + c.w;
+    }
+    float *f = fb + (size_t)p * 3;
+    f[0] = f[0] + sx;
+    f[1] = f[1] + sy;
+    f[2] = f[2] + sz;
+    if (pass_out) {
+        pass_out[(size_t)p * 3] = sx;
+        pass_out[(size_t)p * 3 + 1] = sy;
+        pass_out[(size_t)p * 3 + 2] = sz;
+    }
+}
+
+// ---------------------------------------------------------------- bloom (raytracing.cu:21-74)
+__global__ __launch_bounds__(kBlock) void high_pass_kernel(const float *__restrict__ img, float *__restrict__ out,
+                                                           float threshold, int pixels) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= pixels) return;
+    const V3 c = v3(img[3 * i], img[3 * i + 1], img[3 * i + 2]);
+    const bool bright = dot(c, v3(0.2126f, 0.7152f, 0.0722f)) > threshold;
+    out[3 * i] = bright ? c.x : 0.0f;
+    out[3 * i + 1] = bright ? c.y : 0.0f;
+    out[3 * i + 2] = bright ? c.z : 0.0f;
+}
+
+template <bool VERTICAL>
+__global__ __launch_bounds__(kBlock) void box_blur_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                          int radius, int w, int h) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= w * h) return;
+    const int x = i % w, y = i / w;
+    float sx = 0, sy = 0, sz = 0;
+    int count = 0;
+    for (int k = -radius; k <= radius; k++) {
+        const int nx = VERTICAL ? x : x + k, ny = VERTICAL ? y + k : y;
+        if (VERTICAL ? (ny >= 0 && ny < h) : (nx >= 0 && nx < w)) {
+            const float *p = in + ((size_t)ny * w + nx) * 3;
+            sx = sx + p[0];
+            sy = sy + p[1];
+            sz = sz + p[2];
+            count++;
+        }
+    }
+    const float k = 1.0f / count;
+    out[3 * i] = k * sx;
+    out[3 * i + 1] = k * sy;
+    out[3 * i + 2] = k * sz;
+}
+
+__global__ __launch_bounds__(kBlock) void add_kernel(float *__restrict__ img, const float *__restrict__ add, int n) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) img[i] = img[i] + add[i];
+}
+
+// ==================================================================== host side
+int hip_fail(hipError_t e, const char *what) {
+    return rtamd::fail(e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP,
+                       std::string("Error ") + what + " " + hipGetErrorString(e));
+}
+#define HIPCHK(call)                                          \
+    do {                                                      \
+        const hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #call);     \
+    } while (0)
+
+inline int blocks_for(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    int alloc(size_t count) {
+        if (p) { (void)hipFree(p); p = nullptr; }
+        n = count;
+        if (!count) return RT_OK;
+        HIPCHK(hipMalloc(reinterpret_cast<void **>(&p), count * sizeof(T)));
+        return RT_OK;
+    }
+    int upload(const void *src, size_t count, hipStream_t s) {
+        int rc = alloc(count);
+        if (rc) return rc;
+        if (count) HIPCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+        return RT_OK;
+    }
+};
+
+bool is_leaf(const rt_bvh_node &nd) { return nd.child2 <= nd.child1; }   // scene.cu:859
+
+}  // namespace
+
+struct rt_renderer {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool sort = true, counters = false;
+    int width = 0, height = 0, spp = 0, bounces = 0;
+    DevScene ds{};
+    DevBuf<float4> spheres, tris, mats, nodes, rays;
+    DevBuf<uint16_t> mat_idx;
+    DevBuf<int2> big;
+    DevBuf<float> env, fb;
+    DevBuf<uint32_t> idx[2], sort_counts, sort_offsets, sort_totals;
+    DevBuf<uint8_t> bkt[2];
+    DevBuf<Counters> ctr;
+    std::vector<hipEvent_t> events;
+    hipEvent_t t_begin = nullptr, t_end = nullptr;
+
+    ~rt_renderer() {
+        for (auto e : events) (void)hipEventDestroy(e);
+        if (t_begin) (void)hipEventDestroy(t_begin);
+        if (t_end) (void)hipEventDestroy(t_end);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    int pass_count() const { return (spp + 19) / 20; }
+
+    int init(const rt_scene *sc, const rt_opts *o) {
+        device = o->device;
+        sort = o->sort != 0;
+        counters = o->collect_counters != 0;
+        width = sc->width;
+        height = sc->height;
+        spp = sc->ray_count;
+        bounces = sc->bounces;
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreate(&t_begin));
+        HIPCHK(hipEventCreate(&t_end));
+        int rc;
+        // Child-pair node records (see file header).  Internal nodes keep the reference's
+        // depth-first order, so a subtree's records stay contiguous.
+        const int nn = sc->bvh_node_count;
+        std::vector<int> rec(nn, -1);
+        int nrec = 0;
+        for (int i = 0; i < nn; i++)
+            if (!is_leaf(sc->bvh[i])) rec[i] = nrec++;
+        std::vector<int2> big_h;
+        auto ref_of = [&](int c) -> uint32_t {
+            const rt_bvh_node &nd = sc->bvh[c];
+            if (!is_leaf(nd)) return (uint32_t)rec[c];
+            const int begin = nd.child2, count = nd.child1 - nd.child2;
+            if (count < 64 && begin < (1 << 24)) return kLeaf | ((uint32_t)count << 24) | (uint32_t)begin;
+            big_h.push_back(make_int2(nd.child2, nd.child1));
+            return kLeaf | kBigLeaf | (uint32_t)(big_h.size() - 1);
+        };
+        std::vector<float4> rec_h((size_t)std::max(nrec, 1) * 4);
+        for (int i = 0; i < nn; i++) {
+            if (rec[i] < 0) continue;
+            const rt_bvh_node &nd = sc->bvh[i];
+            if (nd.child1 < 0 || nd.child2 >= nn) return rtamd::fail(RT_E_INVALID, "BVH child index out of range");
+            const rt_bvh_node &l = sc->bvh[nd.child1], &r = sc->bvh[nd.child2];
+            float4 *q = &rec_h[(size_t)rec[i] * 4];
+            q[0] = make_float4(l.min_bound.x, l.min_bound.y, l.min_bound.z, l.max_bound.x);
+            q[1] = make_float4(l.max_bound.y, l.max_bound.z, r.min_bound.x, r.min_bound.y);
+            q[2] = make_float4(r.min_bound.z, r.max_bound.x, r.max_bound.y, r.max_bound.z);
+            const uint32_t a = ref_of(nd.child1), b = ref_of(nd.child2);
+            std::memcpy(&q[3].x, &a, 4);
+            std::memcpy(&q[3].y, &b, 4);
+            q[3].z = q[3].w = 0.0f;
+        }
+        ds.root_ref = nn > 0 ? ref_of(0) : (kLeaf | 0u);
+        if (big_h.empty()) big_h.push_back(make_int2(0, 0));
+        if ((rc = spheres.upload(sc->spheres, sc->sphere_count, stream))) return rc;
+        if ((rc = tris.upload(sc->triangles, (size_t)sc->triangle_count * 3, stream))) return rc;
+        if ((rc = mats.upload(sc->materials, (size_t)sc->material_count * 3, stream))) return rc;
+        if ((rc = mat_idx.upload(sc->material_indices, (size_t)sc->sphere_count + sc->triangle_count, stream))) return rc;
+        if ((rc = nodes.upload(rec_h.data(), rec_h.size(), stream))) return rc;
+        if ((rc = big.upload(big_h.data(), big_h.size(), stream))) return rc;
+        if ((rc = env.upload(sc->environment_map, (size_t)sc->environment_map_width * sc->environment_map_height * 3, stream)))
+            return rc;
+        const int64_t pixels = (int64_t)width * height;
+        const int64_t max_rays = pixels * 20;
+        if (max_rays > 0x7fffffff / 3) return rtamd::fail(RT_E_INVALID, "image too large for 32-bit ray indices");
+        if ((rc = fb.alloc((size_t)pixels * 3))) return rc;
+        if ((rc = rays.alloc((size_t)max_rays * 3))) return rc;
+        for (int k = 0; k < 2; k++) {
+            if ((rc = idx[k].alloc((size_t)max_rays))) return rc;
+            if ((rc = bkt[k].alloc((size_t)max_rays))) return rc;
+            if (!sort) break;
+        }
+        const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
+        if (sort) {
+            if ((rc = sort_counts.alloc((size_t)kBuckets * tiles))) return rc;
+            if ((rc = sort_offsets.alloc((size_t)kBuckets * tiles))) return rc;
+            if ((rc = sort_totals.alloc(kBuckets))) return rc;
+        }
+        if ((rc = ctr.alloc(1))) return rc;
+        HIPCHK(hipMemsetAsync(fb.p, 0, fb.n * sizeof(float), stream));
+        ds.spheres = spheres.p;
+        ds.tris = tris.p;
+        ds.mat_idx = mat_idx.p;
+        ds.mats = mats.p;
+        ds.nodes = nodes.p;
+        ds.big_leaves = big.p;
+        ds.env = env.p;
+        ds.sphere_count = sc->sphere_count;
+        ds.env_w = sc->environment_map_width;
+        ds.env_h = sc->environment_map_height;
+        ds.width = width;
+        ds.height = height;
+        ds.cam = v3(sc->camera_position.x, sc->camera_position.y, sc->camera_position.z);
+        ds.tl = v3(sc->near_plane_top_left.x, sc->near_plane_top_left.y, sc->near_plane_top_left.z);
+        ds.sr = v3(sc->scaled_right.x, sc->scaled_right.y, sc->scaled_right.z);
+        ds.su = v3(sc->scaled_up.x, sc->scaled_up.y, sc->scaled_up.z);
+        ds.min_coord = v3(sc->min_coord.x, sc->min_coord.y, sc->min_coord.z);
+        ds.inv_dim = v3(sc->inv_dimensions.x, sc->inv_dimensions.y, sc->inv_dimensions.z);
+        ds.inv_w = sc->inv_width;
+        ds.inv_h = sc->inv_height;
+        HIPCHK(hipStreamSynchronize(stream));
+        return RT_OK;
+    }
+
+    hipEvent_t event(size_t k) {
+        while (events.size() <= k) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            events.push_back(e);
+        }
+        return events[k];
+    }
+
+    // Pass p of `while (remaining_rays)` (raytracing.cu:222-254).
+    int run_pass(int p, float *pass_out, size_t &ev, int64_t &sorted) {
+        const int before = spp - 20 * p;
+        const int rtc = std::min(before, 20);
+        const int remaining = before - rtc;
+        const int64_t pixels = (int64_t)width * height;
+        const int n = (int)(rtc * pixels);
+        const int grid = blocks_for(n);
+        const int tiles = (n + kSortTile - 1) / kSortTile;
+        int cur = 0;
+        hipLaunchKernelGGL(generate_kernel, dim3(grid), dim3(kBlock), 0, stream, ds, rays.p, idx[0].p, bkt[0].p, rtc, n,
+                           709579u * (uint32_t)remaining);
+        for (int b = 0; b < bounces; b++) {
+            const uint32_t seed_term = 279220567u * (uint32_t)(remaining * 20 + b);
+            hipEvent_t e0 = event(ev++), e1 = event(ev++);
+            if (!e0 || !e1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
+            HIPCHK(hipEventRecord(e0, stream));
+            if (sort) {
+                if (counters)
+                    hipLaunchKernelGGL((process_kernel<true, true>), dim3(grid), dim3(kBlock), 0, stream, ds, rays.p,
+                                       idx[cur].p, bkt[cur].p, n, seed_term, ctr.p);
+                else
+                    hipLaunchKernelGGL((process_kernel<true, false>), dim3(grid), dim3(kBlock), 0, stream, ds, rays.p,
+                                       idx[cur].p, bkt[cur].p, n, seed_term, ctr.p);
+            } else {
+                if (counters)
+                    hipLaunchKernelGGL((process_kernel<false, true>), dim3(grid), dim3(kBlock), 0, stream, ds, rays.p,
+                                       idx[cur].p, bkt[cur].p, n, seed_term, ctr.p);
+                else
+                    hipLaunchKernelGGL((process_kernel<false, false>), dim3(grid), dim3(kBlock), 0, stream, ds, rays.p,
+                                       idx[cur].p, bkt[cur].p, n, seed_term, ctr.p);
+            }
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(e1, stream));
+            if (sort && b + 1 != bounces) {
+                hipEvent_t s0 = event(ev++), s1 = event(ev++);
+                if (!s0 || !s1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
+                HIPCHK(hipEventRecord(s0, stream));
+                hipLaunchKernelGGL(sort_hist_kernel, dim3(tiles), dim3(kBlock), 0, stream, bkt[cur].p, n, tiles,
+                                   sort_counts.p);
+                hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, stream, sort_counts.p, tiles,
+                                   sort_offsets.p, sort_totals.p);
+                hipLaunchKernelGGL(sort_scatter_kernel, dim3(tiles), dim3(kBlock), 0, stream, bkt[cur].p, idx[cur].p, n,
+                                   tiles, sort_offsets.p, sort_totals.p, bkt[1 - cur].p, idx[1 - cur].p);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(s1, stream));
+                cur = 1 - cur;
+                sorted += n;
+            }
+        }
+        hipLaunchKernelGGL(accumulate_kernel, dim3(blocks_for(pixels)), dim3(kBlock), 0, stream, fb.p, rays.p, rtc,
+                           (int)pixels, pass_out);
+        HIPCHK(hipGetLastError());
+        return RT_OK;
+    }
+
+    int run(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st) {
+        const auto w0 = std::chrono::high_resolution_clock::now();
+        HIPCHK(hipSetDevice(device));
+        if (stride < 1) stride = 1;
+        const int P = pass_count();
+        if (count < 0) count = pass_begin < P ? (P - pass_begin + stride - 1) / stride : 0;
+        if (pass_begin < 0 || (count > 0 && pass_begin + (int64_t)(count - 1) * stride >= P))
+            return rtamd::fail(RT_E_INVALID, "pass range outside the render");
+        HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters), stream));
+        HIPCHK(hipEventRecord(t_begin, stream));
+        size_t ev = 0;
+        int64_t sorted = 0, generated = 0;
+        const int64_t pixels = (int64_t)width * height;
+        for (int k = 0; k < count; k++) {
+            const int p = pass_begin + k * stride;
+            const int rc = run_pass(p, pass_sums ? pass_sums + (size_t)k * pixels * 3 : nullptr, ev, sorted);
+            if (rc) return rc;
+            generated += (int64_t)std::min(spp - 20 * p, 20) * pixels;
+        }
+        HIPCHK(hipEventRecord(t_end, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        if (st) {
+            std::memset(st, 0, sizeof(*st));
+            Counters c;
+            HIPCHK(hipMemcpy(&c, ctr.p, sizeof(c), hipMemcpyDeviceToHost));
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, t_begin, t_end));
+            st->kernel_ms = ms;
+            // Events come in (process begin, end) pairs, with (sort begin, end) pairs between.
+            double proc = 0, srt = 0;
+            size_t k = 0;
+            for (int q = 0; q < count; q++)
+                for (int b = 0; b < bounces; b++) {
+                    HIPCHK(hipEventElapsedTime(&ms, events[k], events[k + 1]));
+                    proc += ms;
+                    k += 2;
+                    if (sort && b + 1 != bounces) {
+                        HIPCHK(hipEventElapsedTime(&ms, events[k], events[k + 1]));
+                        srt += ms;
+                        k += 2;
+                    }
+                }
+            st->process_ms = proc;
+            st->sort_ms = srt;
+            st->generated_rays = (uint64_t)generated;
+            st->live_segments = c.live;
+            st->sorted_items = (uint64_t)sorted;
+            st->nodes_popped = c.pn;
+            st->internal_visits = c.iv;
+            st->triangle_tests = c.tt;
+            st->sphere_tests = c.st;
+            st->hits = c.hits;
+            st->misses = c.misses;
+            st->passes = (uint32_t)count;
+            st->render_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
+        }
+        return RT_OK;
+    }
+};
+
+namespace {
+
+int check_scene(const rt_scene *s) {
+    if (!s) return rtamd::fail(RT_E_INVALID, "null scene");
+    if (s->width < 2 || s->height < 2 || s->ray_count < 0 || s->bounces < 0)
+        return rtamd::fail(RT_E_INVALID, "scene image must be at least 2x2 with non-negative spp/bounces");
+    if (s->bvh_node_count < 1 || !s->bvh) return rtamd::fail(RT_E_INVALID, "scene has no BVH root");
+    if (s->environment_map_width < 1 || s->environment_map_height < 1 || !s->environment_map)
+        return rtamd::fail(RT_E_INVALID, "scene has no environment map");
+    if ((s->sphere_count && !s->spheres) || (s->triangle_count && !s->triangles) || !s->materials ||
+        (s->sphere_count + s->triangle_count && !s->material_indices))
+        return rtamd::fail(RT_E_INVALID, "scene array missing");
+    return RT_OK;
+}
+
+int run_bloom(float *d_fb, int w, int h, float threshold, int radius, hipStream_t s) {
+    const int pixels = w * h;
+    float *bright = nullptr, *blur = nullptr;
+    HIPCHK(hipMalloc(reinterpret_cast<void **>(&bright), (size_t)pixels * 3 * sizeof(float)));
+    const hipError_t e = hipMalloc(reinterpret_cast<void **>(&blur), (size_t)pixels * 3 * sizeof(float));
+    if (e != hipSuccess) { (void)hipFree(bright); return hip_fail(e, "hipMalloc(blur)"); }
+    hipLaunchKernelGGL(high_pass_kernel, dim3(blocks_for(pixels)), dim3(kBlock), 0, s, d_fb, bright, threshold, pixels);
+    hipLaunchKernelGGL(box_blur_kernel<false>, dim3(blocks_for(pixels)), dim3(kBlock), 0, s, bright, blur, radius, w, h);
+    hipLaunchKernelGGL(box_blur_kernel<true>, dim3(blocks_for(pixels)), dim3(kBlock), 0, s, blur, bright, radius, w, h);
+    hipLaunchKernelGGL(add_kernel, dim3(blocks_for(pixels * 3)), dim3(kBlock), 0, s, d_fb, bright, pixels * 3);
+    const hipError_t le = hipGetLastError();
+    const hipError_t se = hipStreamSynchronize(s);
+    (void)hipFree(bright);
+    (void)hipFree(blur);
+    if (le != hipSuccess) return hip_fail(le, "bloom launch");
+    if (se != hipSuccess) return hip_fail(se, "bloom sync");
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void rt_default_opts(rt_opts *o) {
+    std::memset(o, 0, sizeof(*o));
+    o->sort = 1;
+    o->pass_count = -1;
+    o->pass_stride = 1;
+}
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer **out) {
+    if (!out) return rtamd::fail(RT_E_INVALID, "null output");
+    *out = nullptr;
+    int rc = check_scene(scene);
+    if (rc) return rc;
+    rt_opts o;
+    if (opts) o = *opts; else rt_default_opts(&o);
+    if (rt_device_count() <= o.device || o.device < 0) return rtamd::fail(RT_E_NODEVICE, "no such HIP device");
+    auto *r = new rt_renderer();
+    rc = r->init(scene, &o);
+    if (rc) { delete r; return rc; }
+    *out = r;
+    return RT_OK;
+}
+
+int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride, float *d_pass_sums,
+                    rt_stats *stats) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    return r->run(pass_begin, count, stride, d_pass_sums, stats);
+}
+
+int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out) {
+    if (!r || !fb_out) return rtamd::fail(RT_E_INVALID, "null argument");
+    HIPCHK(hipSetDevice(r->device));
+    HIPCHK(hipMemcpyAsync(fb_out, r->fb.p, r->fb.n * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+    HIPCHK(hipStreamSynchronize(r->stream));
+    return RT_OK;
+}
+
+int rt_renderer_clear(rt_renderer *r) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    HIPCHK(hipSetDevice(r->device));
+    HIPCHK(hipMemsetAsync(r->fb.p, 0, r->fb.n * sizeof(float), r->stream));
+    HIPCHK(hipStreamSynchronize(r->stream));
+    return RT_OK;
+}
+
+int rt_renderer_set_counters(rt_renderer *r, int32_t enable) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    r->counters = enable != 0;
+    return RT_OK;
+}
+
+void rt_renderer_destroy(rt_renderer *r) { delete r; }
+
+int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stats *stats) {
+    const auto w0 = std::chrono::high_resolution_clock::now();
+    if (!fb_out) return rtamd::fail(RT_E_INVALID, "null framebuffer");
+    rt_opts o;
+    if (opts) o = *opts; else rt_default_opts(&o);
+    rt_renderer *r = nullptr;
+    int rc = rt_renderer_create(scene, &o, &r);
+    if (rc) return rc;
+    rc = r->run(o.pass_begin, o.pass_count, o.pass_stride, nullptr, stats);
+    if (!rc) rc = rt_renderer_read_framebuffer(r, fb_out);
+    delete r;
+    if (!rc && stats)
+        stats->render_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
+    return rc;
+}
+
+int rt_bloom_device(float *d_fb, int32_t w, int32_t h, float threshold, int32_t radius, int32_t device) {
+    if (!d_fb || w <= 0 || h <= 0 || radius < 0) return rtamd::fail(RT_E_INVALID, "rt_bloom_device: bad argument");
+    HIPCHK(hipSetDevice(device));
+    return run_bloom(d_fb, w, h, threshold, radius, nullptr);
+}
+
+int rt_bloom(float *fb, int32_t w, int32_t h, float threshold, int32_t radius, int32_t device) {
+    if (!fb || w <= 0 || h <= 0 || radius < 0) return rtamd::fail(RT_E_INVALID, "rt_bloom: bad argument");
+    if (rt_device_count() <= device || device < 0) return rtamd::fail(RT_E_NODEVICE, "no such HIP device");
+    HIPCHK(hipSetDevice(device));
+    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
+    float *d = nullptr;
+    HIPCHK(hipMalloc(reinterpret_cast<void **>(&d), bytes));
+    hipError_t e = hipMemcpy(d, fb, bytes, hipMemcpyHostToDevice);
+    int rc = e == hipSuccess ? run_bloom(d, w, h, threshold, radius, nullptr) : hip_fail(e, "hipMemcpy H2D");
+    if (!rc) {
+        e = hipMemcpy(fb, d, bytes, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = hip_fail(e, "hipMemcpy D2H");
+    }
+    (void)hipFree(d);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,175 @@
+// cli_main.cpp — `raytracing`, the drop-in for the reference executable (raytracing.cu:305-398).
+//
+//   raytracing <scene file> [no_sort] [cpu] [no_gpu] [no_bvh]
+//              [--image W H spp bounces exposure] [--devices N] [--device K]
+//              [--asset-root DIR] [--out FILE] [--stats FILE]
+//
+// Reference behaviour kept: usage line + exit 1 without a scene, "No raytracing hardware
+// specified" + exit 2 for no_gpu without cpu, unknown words ignored, asset paths relative to
+// the CWD, the same stdout lines, CPU image stacked above the GPU image, output
+// raytracing.png.  Added: the --options above (all optional).  --devices N renders whole
+// 20-spp passes round-robin on N GPUs (one host thread each) and sums the per-pass
+// framebuffers in pass order, so the image is identical to the 1-GPU image.
+#include "rt_abi.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+int die(const char *what) {
+    std::printf("Error %s %s\n", what, rt_last_error());
+    return 1;
+}
+
+struct DeviceResult {
+    int rc = 0;
+    std::string err;
+    std::vector<float> sums;   // [passes on this device][W*H*3]
+    rt_stats stats{};
+};
+
+// Multi-GPU pass sharding: device k renders passes k, k+N, ...; pass sums come back to the
+// host and are added in pass order (bit-identical to one device).
+int render_multi(const rt_scene *s, int sort, int ndev, std::vector<float> &fb, rt_stats *total) {
+    const int P = (s->ray_count + 19) / 20;
+    const size_t px3 = (size_t)s->width * s->height * 3;
+    std::vector<DeviceResult> res(ndev);
+    std::vector<std::thread> th;
+    for (int k = 0; k < ndev; k++) {
+        th.emplace_back([&, k]() {
+            DeviceResult &r = res[k];
+            const int count = k < P ? (P - k + ndev - 1) / ndev : 0;
+            if (!count) return;
+            rt_opts o;
+            rt_default_opts(&o);
+            o.sort = sort;
+            o.device = k;
+            rt_renderer *ren = nullptr;
+            r.rc = rt_renderer_create(s, &o, &ren);
+            if (r.rc) { r.err = rt_last_error(); return; }
+            // Pass sums are written to a device staging buffer by the renderer, one pass per call.
+            r.sums.assign((size_t)count * px3, 0.0f);
+            for (int q = 0; q < count && !r.rc; q++) {
+                r.rc = rt_renderer_clear(ren);
+                rt_stats st;
+                if (!r.rc) r.rc = rt_renderer_run(ren, k + q * ndev, 1, 1, nullptr, &st);
+                if (!r.rc) r.rc = rt_renderer_read_framebuffer(ren, r.sums.data() + (size_t)q * px3);
+                r.stats.live_segments += st.live_segments;
+                r.stats.generated_rays += st.generated_rays;
+                r.stats.kernel_ms += st.kernel_ms;
+                r.stats.process_ms += st.process_ms;
+            }
+            if (r.rc) r.err = rt_last_error();
+            rt_renderer_destroy(ren);
+        });
+    }
+    for (auto &t : th) t.join();
+    for (auto &r : res)
+        if (r.rc) { std::printf("Error rt_renderer %s\n", r.err.c_str()); return r.rc; }
+    fb.assign(px3, 0.0f);
+    for (int p = 0; p < P; p++) {
+        const float *src = res[p % ndev].sums.data() + (size_t)(p / ndev) * px3;
+        for (size_t i = 0; i < px3; i++) fb[i] = fb[i] + src[i];
+    }
+    for (auto &r : res) {
+        total->live_segments += r.stats.live_segments;
+        total->generated_rays += r.stats.generated_rays;
+        total->kernel_ms = std::max(total->kernel_ms, r.stats.kernel_ms);
+    }
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    if (argc < 2) {
+        std::printf("Usage: %s <scene>\n", argv[0]);
+        return 1;
+    }
+    bool sort = true, cpu = false, gpu = true, bvh = true;
+    int devices = 1, device = 0;
+    const char *asset_root = nullptr, *out_path = "raytracing.png", *stats_path = nullptr;
+    rt_load_opts lo;
+    rt_default_load_opts(&lo);
+    for (int i = 2; i < argc; i++) {
+        const std::string a = argv[i];
+        if (a == "no_sort") sort = false;
+        else if (a == "cpu") cpu = true;
+        else if (a == "no_bvh") bvh = false;
+        else if (a == "no_gpu") gpu = false;
+        else if (a == "--image" && i + 5 < argc) {
+            lo.image_override = 1;
+            lo.width = std::atoi(argv[++i]);
+            lo.height = std::atoi(argv[++i]);
+            lo.ray_count = std::atoi(argv[++i]);
+            lo.bounces = std::atoi(argv[++i]);
+            lo.exposure_override = 1;
+            lo.exposure = (float)std::atof(argv[++i]);
+        } else if (a == "--devices" && i + 1 < argc) devices = std::max(1, std::atoi(argv[++i]));
+        else if (a == "--device" && i + 1 < argc) device = std::atoi(argv[++i]);
+        else if (a == "--asset-root" && i + 1 < argc) asset_root = argv[++i];
+        else if (a == "--out" && i + 1 < argc) out_path = argv[++i];
+        else if (a == "--stats" && i + 1 < argc) stats_path = argv[++i];
+        // unknown words are ignored, like the reference
+    }
+    if (!cpu && !gpu) {
+        std::printf("No raytracing hardware specified\n");
+        return 2;
+    }
+    lo.use_bvh = bvh ? 1 : 0;
+    lo.asset_root = asset_root;
+    rt_scene_host *host = nullptr;
+    if (rt_scene_load(argv[1], &lo, &host)) return die("load_scene");
+    const rt_scene *s = rt_scene_view(host);
+    const size_t px3 = (size_t)s->width * s->height * 3;
+    std::vector<uint8_t> image;
+    std::vector<float> fb(px3);
+    rt_stats gst{};
+    double cpu_s = 0;
+    if (cpu) {
+        if (rt_cpu_render(s, fb.data(), 0, &cpu_s) < 0) return die("cpu_raytrace");
+        std::printf("CPU Took %gs\n", cpu_s);
+        std::vector<uint8_t> part(px3);
+        rt_tonemap(fb.data(), s->width, s->height, s->exposure, s->ray_count, part.data());
+        image.insert(image.end(), part.begin(), part.end());
+    }
+    if (gpu) {
+        if (devices > 1) {
+            if (render_multi(s, sort ? 1 : 0, devices, fb, &gst)) return 1;
+        } else {
+            rt_opts o;
+            rt_default_opts(&o);
+            o.sort = sort ? 1 : 0;
+            o.device = device;
+            if (rt_render(s, &o, fb.data(), &gst)) return die("gpu_raytrace");
+        }
+        std::printf("GPU Took %gs\n", gst.render_ms / 1000.0);
+        if (rt_bloom(fb.data(), s->width, s->height, (float)(0.7 * s->ray_count), 5, device)) return die("bloom");
+        std::vector<uint8_t> part(px3);
+        rt_tonemap(fb.data(), s->width, s->height, s->exposure, s->ray_count, part.data());
+        image.insert(image.end(), part.begin(), part.end());
+    }
+    if (rt_write_png(out_path, image.data(), s->width, (int)(image.size() / s->width / 3))) return die("stbi_write_png");
+    if (stats_path) {
+        if (FILE *f = std::fopen(stats_path, "w")) {
+            const double secs = gst.render_ms / 1000.0;
+            std::fprintf(f,
+                         "{\"scene\": \"%s\", \"width\": %d, \"height\": %d, \"spp\": %d, \"bounces\": %d, "
+                         "\"sort\": %d, \"devices\": %d, \"render_ms\": %.3f, \"kernel_ms\": %.3f, "
+                         "\"live_segments\": %llu, \"generated_rays\": %llu, \"live_mrays_per_s\": %.3f, "
+                         "\"cpu_s\": %.6f, \"bvh_ms\": %.3f}\n",
+                         argv[1], s->width, s->height, s->ray_count, s->bounces, sort ? 1 : 0, devices, gst.render_ms,
+                         gst.kernel_ms, (unsigned long long)gst.live_segments, (unsigned long long)gst.generated_rays,
+                         secs > 0 ? gst.live_segments / secs / 1e6 : 0.0, cpu_s, rt_scene_bvh_ms(host));
+            std::fclose(f);
+        }
+    }
+    rt_scene_free(host);
+    return 0;
+}

@@ -1,0 +1,283 @@
+"""ctypes host binding of librtamd.so (include/rt_abi.h) for Python callers.
+
+This is plumbing for tests, the benchmark and the multi-GPU driver: every render call goes
+through the C ABI into the HIP kernels.  There is no Python or CPU fallback for the GPU
+path: if the library or a HIP device is missing, the calls raise.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+BUILD_DIR = os.path.join(PKG_DIR, "build")
+LIB_PATH = os.path.join(BUILD_DIR, "librtamd.so")
+CLI_PATH = os.path.join(BUILD_DIR, "raytracing")
+HEADER = os.path.join(REPO, "include", "rt_abi.h")
+ASSETS = os.path.join(REPO, "assets")
+
+
+class RtError(RuntimeError):
+    pass
+
+
+class Vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+P = C.c_void_p
+I32 = C.c_int32
+
+
+class RtScene(C.Structure):
+    _fields_ = [("spheres", P), ("sphere_count", I32), ("triangles", P), ("triangle_count", I32),
+                ("material_indices", P), ("materials", P), ("material_count", I32),
+                ("bvh", P), ("bvh_node_count", I32), ("width", I32), ("height", I32),
+                ("environment_map", P), ("environment_map_width", I32), ("environment_map_height", I32),
+                ("camera_position", Vec3), ("forward", Vec3), ("up", Vec3),
+                ("vertical_fov", C.c_float), ("exposure", C.c_float),
+                ("min_coord", Vec3), ("inv_dimensions", Vec3),
+                ("scaled_right", Vec3), ("scaled_up", Vec3), ("near_plane_top_left", Vec3),
+                ("inv_width", C.c_float), ("inv_height", C.c_float),
+                ("bounces", I32), ("ray_count", I32)]
+
+
+class RtLoadOpts(C.Structure):
+    _fields_ = [("use_bvh", I32), ("quiet", I32), ("asset_root", C.c_char_p), ("image_override", I32),
+                ("width", I32), ("height", I32), ("ray_count", I32), ("bounces", I32),
+                ("exposure_override", I32), ("exposure", C.c_float)]
+
+
+class RtOpts(C.Structure):
+    _fields_ = [("sort", I32), ("device", I32), ("pass_begin", I32), ("pass_count", I32),
+                ("pass_stride", I32), ("collect_counters", I32)]
+
+
+class RtStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("generated_rays", "live_segments", "sorted_items",
+                                          "nodes_popped", "internal_visits", "triangle_tests",
+                                          "sphere_tests", "hits", "misses")] + \
+               [("passes", C.c_uint32), ("reserved", C.c_uint32)] + \
+               [(n, C.c_double) for n in ("render_ms", "kernel_ms", "process_ms", "sort_ms")]
+
+    def as_dict(self):
+        return {n: (float(getattr(self, n)) if t is C.c_double else int(getattr(self, n)))
+                for n, t in self._fields_ if n != "reserved"}
+
+
+_lib = None
+
+
+def build(jobs=8):
+    subprocess.run(["make", "-s", "-j%d" % jobs, "-C", PKG_DIR], check=True)
+
+
+def lib():
+    """Load librtamd.so.  Raises if it has not been built: no fallback exists."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RtError("librtamd.so is not built (run `make -C cuda-raytracer_amd` or "
+                          "__graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        L.rt_last_error.restype = C.c_char_p
+        L.rt_abi_version.restype = C.c_int
+        L.rt_device_count.restype = C.c_int
+        L.rt_default_opts.argtypes = [P]
+        L.rt_default_load_opts.argtypes = [P]
+        L.rt_scene_load.argtypes = [C.c_char_p, P, C.POINTER(P)]
+        L.rt_scene_view.argtypes = [P]
+        L.rt_scene_view.restype = C.POINTER(RtScene)
+        L.rt_scene_bvh_ms.argtypes = [P]
+        L.rt_scene_bvh_ms.restype = C.c_double
+        L.rt_scene_free.argtypes = [P]
+        L.rt_render.argtypes = [P, P, P, P]
+        L.rt_renderer_create.argtypes = [P, P, C.POINTER(P)]
+        L.rt_renderer_run.argtypes = [P, I32, I32, I32, P, P]
+        L.rt_renderer_read_framebuffer.argtypes = [P, P]
+        L.rt_renderer_clear.argtypes = [P]
+        L.rt_renderer_set_counters.argtypes = [P, I32]
+        L.rt_renderer_destroy.argtypes = [P]
+        L.rt_bloom.argtypes = [P, I32, I32, C.c_float, I32, I32]
+        L.rt_bloom_device.argtypes = [P, I32, I32, C.c_float, I32, I32]
+        L.rt_tonemap.argtypes = [P, I32, I32, C.c_float, I32, P]
+        L.rt_write_png.argtypes = [C.c_char_p, P, I32, I32]
+        L.rt_cpu_render.argtypes = [P, P, I32, C.POINTER(C.c_double)]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RtError("rt error %d: %s" % (rc, lib().rt_last_error().decode()))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(P)
+
+
+def device_count():
+    return lib().rt_device_count()
+
+
+class Scene:
+    """A scene loaded by the product loader (rt_scene_load)."""
+
+    def __init__(self, path, use_bvh=True, asset_root=ASSETS, image=None, exposure=None, quiet=True):
+        L = lib()
+        o = RtLoadOpts()
+        L.rt_default_load_opts(C.byref(o))
+        o.use_bvh = int(use_bvh)
+        o.quiet = int(quiet)
+        self._root = asset_root.encode() if asset_root else None
+        o.asset_root = self._root
+        if image is not None:
+            o.image_override = 1
+            o.width, o.height, o.ray_count, o.bounces = [int(v) for v in image]
+        if exposure is not None:
+            o.exposure_override = 1
+            o.exposure = float(exposure)
+        h = P()
+        _check(L.rt_scene_load(path.encode(), C.byref(o), C.byref(h)))
+        self.h = h
+        self.view = L.rt_scene_view(h).contents
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rt_scene_free(self.h)
+            self.h = None
+
+    @property
+    def ptr(self):
+        return lib().rt_scene_view(self.h)
+
+    @property
+    def width(self):
+        return self.view.width
+
+    @property
+    def height(self):
+        return self.view.height
+
+    @property
+    def pixels(self):
+        return self.view.width * self.view.height
+
+    @property
+    def passes(self):
+        return (self.view.ray_count + 19) // 20
+
+    @property
+    def bvh_ms(self):
+        return lib().rt_scene_bvh_ms(self.h)
+
+    def arrays(self):
+        v = self.view
+
+        def arr(p, n, cols, dt=np.float32):
+            if n == 0:
+                return np.zeros((0, cols) if cols else 0, dt)
+            itemsize = np.dtype(dt).itemsize * (cols or 1)
+            buf = (C.c_char * (n * itemsize)).from_address(p)
+            a = np.frombuffer(buf, dtype=dt).copy()
+            return a.reshape(n, cols) if cols else a
+        cam = np.array([v.camera_position.x, v.camera_position.y, v.camera_position.z,
+                        v.forward.x, v.forward.y, v.forward.z, v.up.x, v.up.y, v.up.z,
+                        v.vertical_fov] +
+                       [c for vec in (v.min_coord, v.inv_dimensions, v.scaled_right, v.scaled_up,
+                                      v.near_plane_top_left) for c in (vec.x, vec.y, vec.z)] +
+                       [v.inv_width, v.inv_height, v.exposure, 0.0, 0.0], dtype=np.float32)
+        return dict(spheres=arr(v.spheres, v.sphere_count, 4),
+                    triangles=arr(v.triangles, v.triangle_count, 12),
+                    material_indices=arr(v.material_indices, v.sphere_count + v.triangle_count, 0, np.uint16),
+                    materials=arr(v.materials, v.material_count, 12),
+                    bvh=arr(v.bvh, v.bvh_node_count, 8),
+                    env=arr(v.environment_map, v.environment_map_width * v.environment_map_height, 3),
+                    camera=cam)
+
+
+def default_opts(sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=1, counters=False):
+    o = RtOpts()
+    lib().rt_default_opts(C.byref(o))
+    o.sort, o.device, o.pass_begin, o.pass_count = int(sort), device, pass_begin, pass_count
+    o.pass_stride, o.collect_counters = pass_stride, int(counters)
+    return o
+
+
+def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=1, counters=False):
+    """rt_render: the drop-in for gpu_raytrace.  Returns (framebuffer W*H*3 float32, stats)."""
+    fb = np.zeros(scene.pixels * 3, np.float32)
+    st = RtStats()
+    o = default_opts(sort, device, pass_begin, pass_count, pass_stride, counters)
+    _check(lib().rt_render(scene.ptr, C.byref(o), _ptr(fb), C.byref(st)))
+    return fb, st.as_dict()
+
+
+class Renderer:
+    """Persistent renderer (scene + ray buffers resident in HBM)."""
+
+    def __init__(self, scene, sort=True, device=0, counters=False):
+        self.scene = scene
+        o = default_opts(sort, device, counters=counters)
+        h = P()
+        _check(lib().rt_renderer_create(scene.ptr, C.byref(o), C.byref(h)))
+        self.h = h
+
+    def run(self, pass_begin=0, count=1, stride=1, d_pass_sums=None):
+        st = RtStats()
+        _check(lib().rt_renderer_run(self.h, pass_begin, count, stride,
+                                     P(d_pass_sums) if d_pass_sums else None, C.byref(st)))
+        return st.as_dict()
+
+    def set_counters(self, on):
+        _check(lib().rt_renderer_set_counters(self.h, int(on)))
+
+    def framebuffer(self):
+        fb = np.zeros(self.scene.pixels * 3, np.float32)
+        _check(lib().rt_renderer_read_framebuffer(self.h, _ptr(fb)))
+        return fb
+
+    def clear(self):
+        _check(lib().rt_renderer_clear(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rt_renderer_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def bloom(fb, width, height, threshold, radius=5, device=0):
+    out = np.array(fb, dtype=np.float32, copy=True)
+    _check(lib().rt_bloom(_ptr(out), width, height, threshold, radius, device))
+    return out
+
+
+def bloom_device(ptr, width, height, threshold, radius=5, device=0):
+    _check(lib().rt_bloom_device(P(ptr), width, height, threshold, radius, device))
+
+
+def tonemap(fb, width, height, exposure, ray_count):
+    out = np.zeros(width * height * 3, np.uint8)
+    src = np.ascontiguousarray(fb, dtype=np.float32)
+    lib().rt_tonemap(_ptr(src), width, height, exposure, ray_count, _ptr(out))
+    return out
+
+
+def write_png(path, rgb, width, height):
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    _check(lib().rt_write_png(path.encode(), _ptr(rgb), width, height))
+
+
+def cpu_render(scene, threads=0):
+    """The reference's `cpu` path (rt_cpu_render). Returns (fb, seconds)."""
+    fb = np.zeros(scene.pixels * 3, np.float32)
+    secs = C.c_double(0)
+    rc = lib().rt_cpu_render(scene.ptr, _ptr(fb), threads, C.byref(secs))
+    if rc < 0:
+        raise RtError(lib().rt_last_error().decode())
+    return fb, secs.value

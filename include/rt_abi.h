@@ -1,0 +1,168 @@
+/*
+ * rt_abi.h — C ABI of the MI355X-native path tracer (librtamd.so).
+ *
+ * Drop-in boundary for isaac-chandler/cuda-raytracer's GPU render path.  Plain C types,
+ * pointers and sizes only; no HIP or torch types cross this boundary.  Every entry point
+ * names the reference interface it replaces (file:line in the reference checkout).
+ *
+ * Byte layouts of the scene arrays are the reference's (scene.cuh:9-100):
+ *   rt_sphere 16 B, rt_triangle 48 B (ray-tracing representation: p1, p2-p1, p3-p1,
+ *   normalise(cross(p3-p1, p2-p1))), rt_material 48 B, rt_bvh_node 32 B,
+ *   uint16 material indices (spheres first, then triangles), env map float[h][w][3].
+ *
+ * Errors: every int-returning call returns 0 on success or a negative RT_E_* code and
+ * records a message readable with rt_last_error() (thread-local).  The reference printed
+ * "Error <expr> <msg>" and exit(1) instead (common.cuh:10-18); the CLI keeps that.
+ * Threading: calls are blocking.  One rt_renderer is bound to one device and must not be
+ * used from two threads at once; distinct renderers may run concurrently.
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_E_INVALID = -1,   /* bad argument / scene */
+    RT_E_IO = -2,        /* file could not be read or written */
+    RT_E_HIP = -3,       /* HIP runtime error (message has the HIP error string) */
+    RT_E_NODEVICE = -4,  /* no HIP device / HIP kernels not loadable */
+    RT_E_OOM = -5        /* device allocation failed */
+};
+
+typedef struct { float x, y, z; } rt_vec3;
+typedef struct { rt_vec3 center; float radius; } rt_sphere;                          /* scene.cuh:9  */
+typedef struct { rt_vec3 p1, p2p1, p3p1, normal; } rt_triangle;                      /* scene.cuh:27 */
+typedef struct {                                                                      /* scene.cuh:42 */
+    rt_vec3 diffuse_albedo; float metallicity;
+    rt_vec3 specular_albedo; float roughness;
+    rt_vec3 emitted; float index_of_refraction;
+} rt_material;
+typedef struct { rt_vec3 min_bound, max_bound; int32_t child1, child2; } rt_bvh_node; /* scene.cuh:82 */
+
+/* Host view of a loaded scene; mirrors `struct Scene` (scene.cuh:102-152). All pointers are
+ * borrowed host memory. */
+typedef struct {
+    const rt_sphere *spheres;         int32_t sphere_count;
+    const rt_triangle *triangles;     int32_t triangle_count;
+    const uint16_t *material_indices;
+    const rt_material *materials;     int32_t material_count;
+    const rt_bvh_node *bvh;           int32_t bvh_node_count;
+    int32_t width, height;
+    const rt_vec3 *environment_map;   int32_t environment_map_width, environment_map_height;
+    rt_vec3 camera_position, forward, up;
+    float vertical_fov, exposure;
+    rt_vec3 min_coord, inv_dimensions;
+    rt_vec3 scaled_right, scaled_up, near_plane_top_left;
+    float inv_width, inv_height;
+    int32_t bounces, ray_count;
+} rt_scene;
+
+/* ------------------------------------------------------------------ scene loading (host)
+ * Replaces load_scene(Scene*, const char*, bool use_bvh) (scene.cu:569-831) including
+ * load_ply (:491), load_pfm (:548), precompute_camera_data (:62) and the binned-SAH
+ * generate_bvh (:1002-1036).  CRLF scene files are accepted (the reference read them in
+ * Windows text mode).  Prints the reference's stdout lines unless opts->quiet. */
+typedef struct {
+    int32_t use_bvh;          /* 1 = BVH depth 30 (default); 0 = `no_bvh` (single leaf)      */
+    int32_t quiet;            /* 1 = suppress "Triangle count"/"BVH Took"/... stdout lines      */
+    const char *asset_root;   /* directory relative asset paths resolve against; NULL = CWD  */
+    int32_t image_override;   /* 1 = replace the scene's `image` W H spp bounces with below   */
+    int32_t width, height, ray_count, bounces;
+    int32_t exposure_override;
+    float exposure;
+} rt_load_opts;
+
+typedef struct rt_scene_host rt_scene_host;   /* owns the arrays a rt_scene points into */
+
+int rt_scene_load(const char *path, const rt_load_opts *opts, rt_scene_host **out);
+const rt_scene *rt_scene_view(const rt_scene_host *scene);
+double rt_scene_bvh_ms(const rt_scene_host *scene);          /* "BVH Took" (scene.cu:1026) */
+void rt_scene_free(rt_scene_host *scene);
+
+/* ------------------------------------------------------------------ GPU render
+ * Pass p (0-based) of a render casts rtc = min(spp - 20p, 20) rays per pixel with
+ * generate-seed `remaining` = spp - 20p - rtc (raytracing.cu:222-229). */
+typedef struct {
+    int32_t sort;         /* 1 = ray reordering after each bounce but the last (default);
+                             0 = `no_sort` (raytracing.cu:238)                             */
+    int32_t device;       /* HIP device ordinal                                          */
+    int32_t pass_begin;   /* first pass to render (0)                                    */
+    int32_t pass_count;   /* passes to render; -1 = all remaining                        */
+    int32_t pass_stride;  /* render passes pass_begin, +stride, ... (multi-GPU pass shard) */
+    int32_t collect_counters; /* 1 = also count traversal work (Pn/Iv/Tt) for the byte model */
+} rt_opts;
+
+typedef struct {
+    uint64_t generated_rays;   /* rays generated (sum of n over passes)                    */
+    uint64_t live_segments;    /* process_ray invocations on live slots                    */
+    uint64_t sorted_items;     /* slots moved by the reorder                               */
+    uint64_t nodes_popped;     /* Pn, only with collect_counters                           */
+    uint64_t internal_visits;  /* Iv, only with collect_counters                           */
+    uint64_t triangle_tests;   /* Tt, only with collect_counters                           */
+    uint64_t sphere_tests;     /* S x live segments                                        */
+    uint64_t hits, misses;
+    uint32_t passes, reserved;
+    double render_ms;          /* host wall time of the call (the "GPU Took" span)         */
+    double kernel_ms;          /* HIP-event time of the whole pass loop on the stream      */
+    double process_ms;         /* HIP-event time summed over the process (traversal) launches */
+    double sort_ms;            /* HIP-event time summed over the reorder launches          */
+} rt_stats;
+
+void rt_default_opts(rt_opts *opts);
+void rt_default_load_opts(rt_load_opts *opts);
+int rt_device_count(void);
+
+/* Replaces `Vec3 *gpu_raytrace(const Scene *scene, bool sort)` (raytracing.cu:170-284):
+ * uploads the scene, renders every pass selected by opts, and writes the accumulated
+ * framebuffer (W*H*3 floats, raw radiance sums, caller-owned) to fb_out. */
+int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stats *stats);
+
+/* Persistent renderer: scene resident in HBM, ray buffers sized for 20 rays/pixel.
+ * Used by the benchmark and by the multi-GPU pass-sharded driver. */
+typedef struct rt_renderer rt_renderer;
+int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer **out);
+/* Renders passes pass_begin, pass_begin+stride, ... (count passes) and adds each pass's
+ * per-pixel sum into the renderer's device framebuffer (ordered: fb += pass_sum, pass
+ * order).  If d_pass_sums != NULL (device pointer, count*W*H*3 floats) the pass sums are
+ * also stored there.  Blocking. */
+int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride,
+                    float *d_pass_sums, rt_stats *stats);
+int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out);   /* device fb -> host     */
+int rt_renderer_clear(rt_renderer *r);                               /* zero the device fb    */
+int rt_renderer_set_counters(rt_renderer *r, int32_t enable);
+void rt_renderer_destroy(rt_renderer *r);
+
+/* Replaces the bloom block of main (raytracing.cu:356-393, kernels :21-74): high-pass
+ * (luminance > threshold), clamped box blur of `radius` horizontally then vertically,
+ * add back.  fb is a host W*H*3 buffer, updated in place. */
+int rt_bloom(float *fb, int32_t width, int32_t height, float threshold, int32_t radius, int32_t device);
+/* Same on a device-resident framebuffer (device pointer). */
+int rt_bloom_device(float *d_fb, int32_t width, int32_t height, float threshold, int32_t radius,
+                    int32_t device);
+
+/* Replaces write_framebuffer_to_output_image (raytracing.cu:286-303). rgb_out: W*H*3. */
+void rt_tonemap(const float *fb, int32_t width, int32_t height, float exposure, int32_t ray_count,
+                uint8_t *rgb_out);
+/* Replaces stbi_write_png (raytracing.cu:395): 8-bit RGB PNG, own encoder (lossless). */
+int rt_write_png(const char *path, const uint8_t *rgb, int32_t width, int32_t height);
+
+/* Replaces `Vec3 *cpu_raytrace(Scene *scene)` (raytracing.cu:122-163): the reference's
+ * OpenMP CPU path with its bounce-invariant seed; fb_out W*H*3 (overwritten).  Returns the
+ * number of passes rendered; seconds = the "CPU Took" span. */
+int rt_cpu_render(const rt_scene *scene, float *fb_out, int32_t threads, double *seconds);
+
+const char *rt_last_error(void);
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_ABI_H */

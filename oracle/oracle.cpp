@@ -1,0 +1,1017 @@
+// oracle.cpp — TEST INFRASTRUCTURE ONLY (see oracle.h for the rules and pinning status).
+//
+// A plain C++ restatement of isaac-chandler/cuda-raytracer, written from the reference source
+// text (never compiled or linked against it).  Every function cites the reference lines it
+// follows.  Arithmetic conventions (shared by contract with the HIP kernels, restated there
+// independently):
+//   * IEEE fp32/fp64, no contraction (-ffp-contract=off), no fast-math, no FTZ.
+//   * min/max on floats are C fminf/fmaxf semantics (NaN-ignoring; ties return the first
+//     argument, which only affects the sign of zero and never a comparison result).
+//   * cosf/sinf/atanf are replaced by the deterministic float kernels rt_sincos/rt_atan01
+//     below (the reference used nvcc --use_fast_math __sinf/__cosf: parity unpinned there).
+//   * double sub-expressions are kept where the reference evaluates in double
+//     (random.cuh:44, scene.cu:55-57, 190, 297, 357, 366, 380-381, 389-390).
+//   * float->u16 in morton_code saturates (NaN/<=0 -> 0, >=65535 -> 65535), PTX cvt semantics.
+#include "oracle.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace {
+
+thread_local std::string g_err;
+
+// ---------------------------------------------------------------- math.cuh:11-142
+struct V3 { float x, y, z; };
+static_assert(sizeof(V3) == 12, "Vec3 is 12 B");
+
+inline float fmin_(float a, float b) { if (a != a) return b; if (b != b) return a; return (b < a) ? b : a; }
+inline float fmax_(float a, float b) { if (a != a) return b; if (b != b) return a; return (b > a) ? b : a; }
+inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+inline V3 operator*(float s, V3 v) { return {s * v.x, s * v.y, s * v.z}; }
+inline V3 operator-(V3 v) { return {-v.x, -v.y, -v.z}; }
+inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }           // :67
+inline V3 cross(V3 a, V3 b) {                                                           // :72
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+inline float magsq(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }                  // :82
+inline V3 normalise(V3 v) { return (1.0f / sqrtf(magsq(v))) * v; }                      // :111
+inline float clamp01(float x) { return fmax_(fmin_(x, 1.0f), 0.0f); }                   // :116-124
+inline V3 vmin(V3 a, V3 b) { return {fmin_(a.x, b.x), fmin_(a.y, b.y), fmin_(a.z, b.z)}; }
+inline V3 vmax(V3 a, V3 b) { return {fmax_(a.x, b.x), fmax_(a.y, b.y), fmax_(a.z, b.z)}; }
+inline float comp(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+inline bool is_black(V3 v) { return v.x == 0 && v.y == 0 && v.z == 0; }
+
+// Deterministic replacements for cosf/sinf (random.cuh:63-75) and atanf (scene.cu:297).
+// Cody-Waite reduction by pi/2 + cephes minimax polynomials; valid for x >= 0 (the only use is
+// random_radians in [0, 2*pi]).  Operation order is part of the contract with the HIP kernels.
+inline void rt_sincos(float x, float *s, float *c) {
+    const float fj = x * 0.636619772f;
+    const int j = (int)(fj + 0.5f);
+    const float jf = (float)j;
+    const float r = ((x - jf * 1.5703125f) - jf * 4.837512969970703125e-4f) - jf * 7.54978995489188216e-8f;
+    const float z = r * r;
+    const float sp = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * r + r;
+    const float cp = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z
+                     - 0.5f * z + 1.0f;
+    switch (j & 3) {
+    case 0: *s = sp; *c = cp; break;
+    case 1: *s = cp; *c = -sp; break;
+    case 2: *s = -sp; *c = -cp; break;
+    default: *s = -cp; *c = sp; break;
+    }
+}
+inline float rt_atan01(float x) {
+    float y = 0.0f;
+    if (x > 0.4142135623730950f) { y = 0.78539816339744830962f; x = (x - 1.0f) / (x + 1.0f); }
+    const float z = x * x;
+    return y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z
+                 - 3.33329491539e-1f) * z * x + x);
+}
+
+// ---------------------------------------------------------------- random.cuh:5-75
+struct Rng { uint64_t state, inc; };
+inline uint32_t xor_rand(Rng *r) {                                                     // :13-23
+    const uint64_t old = r->state;
+    r->state = old * 6364136223846793005ULL + (r->inc | 1);
+    const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+    const uint32_t rot = (uint32_t)(old >> 59);
+    return (xs >> rot) | (xs << ((0u - rot) & 31));
+}
+inline void xor_srand(Rng *r, uint32_t seed) {                                         // :25-30
+    r->state = (uint64_t)seed * 6839056345687307ULL;
+    r->inc = 820957824423429ULL;
+    xor_rand(r);
+}
+inline float random01(Rng *r) { return (float)xor_rand(r) * (1.0f / 4294967296.0f); }  // :32-35
+inline float random02(Rng *r) { return (float)xor_rand(r) * (2.0f / 4294967296.0f); }  // :37-40
+inline float random_radians(Rng *r) {                                                  // :42-45 (double)
+    return (float)((double)xor_rand(r) * (3.14159265358979323846 * 2 / 4294967295.0));
+}
+inline V3 random_on_sphere(Rng *r) {                                                   // :63-75
+    const float r1 = random_radians(r);
+    const float r2 = random02(r);
+    const float x = sqrtf(r2 * (2 - r2));
+    float s, c;
+    rt_sincos(r1, &s, &c);
+    return {c * x, s * x, 1 - r2};
+}
+
+// ---------------------------------------------------------------- scene.cuh:9-166
+struct Sphere { V3 center; float radius; };
+struct Triangle { V3 p1, p2p1, p3p1, normal; };
+struct Material { V3 diffuse; float metallicity; V3 specular; float roughness; V3 emitted; float ior; };
+struct RayData { V3 origin, dir, transmitted, collected; };
+struct Aabb {
+    V3 mn{1e30f, 1e30f, 1e30f};
+    V3 mx{-1e30f, -1e30f, -1e30f};
+    void expand(V3 v) { mn = vmin(mn, v); mx = vmax(mx, v); }                          // scene.cu:833
+    void expand(const Triangle &t) { expand(t.p1); expand(t.p2p1); expand(t.p3p1); }    // :839
+    void expand(const Aabb &o) { mn = vmin(mn, o.mn); mx = vmax(mx, o.mx); }            // :846
+    float half_area() const {                                                          // :852
+        const V3 s = mx - mn;
+        return s.x * s.y + s.x * s.z + s.y * s.z;
+    }
+};
+struct BvhNode { Aabb aabb; int32_t child1 = 0, child2 = 0; };
+static_assert(sizeof(Sphere) == 16 && sizeof(Triangle) == 48 && sizeof(Material) == 48, "layouts");
+static_assert(sizeof(BvhNode) == 32 && sizeof(RayData) == 48, "layouts");
+inline bool is_leaf(const BvhNode &n) { return n.child2 <= n.child1; }                 // :859
+
+}  // namespace
+
+struct orc_scene {
+    std::vector<Sphere> spheres;
+    std::vector<Triangle> triangles;
+    std::vector<uint16_t> material_indices;
+    std::vector<Material> materials;
+    std::vector<BvhNode> bvh;
+    std::vector<V3> env;
+    int env_w = 0, env_h = 0;
+    int width = 1920, height = 1080, ray_count = 1, bounces = 3;                        // :571-574
+    float exposure = 0;
+    V3 camera_position{0, 0, 0}, forward{0, 0, 0}, up{0, 0, 0};
+    float vertical_fov = 0;
+    V3 min_coord{0, 0, 0}, inv_dimensions{0, 0, 0};
+    V3 scaled_right{0, 0, 0}, scaled_up{0, 0, 0}, near_plane_top_left{0, 0, 0};
+    float inv_width = 0, inv_height = 0;
+};
+
+namespace {
+
+// ---------------------------------------------------------------- scene.cu:62-76
+void precompute_camera_data(orc_scene *s) {
+    const V3 right = cross(s->up, s->forward);
+    const float nph = 2.0f * std::tan(s->vertical_fov * 0.5f);
+    const float npw = nph * s->width / s->height;
+    s->scaled_right = npw * right;
+    s->scaled_up = nph * s->up;
+    s->near_plane_top_left = s->forward - 0.5f * s->scaled_right + 0.5f * s->scaled_up;
+    s->inv_width = 1.0f / (s->width - 1);
+    s->inv_height = 1.0f / (s->height - 1);
+}
+
+// ---------------------------------------------------------------- scene.cu:866-1000
+void maybe_split(orc_scene *s, int node_index, int max_depth) {
+    std::vector<BvhNode> &nodes = s->bvh;
+    std::vector<Triangle> &tris = s->triangles;
+    const int c2 = nodes[node_index].child2, c1 = nodes[node_index].child1;
+    {
+        Aabb box = nodes[node_index].aabb;
+        for (int i = c2; i < c1; i++) box.expand(tris[i]);
+        nodes[node_index].aabb = box;
+    }
+    const int our_count = c1 - c2;
+    if (our_count <= 4 || max_depth == 0) return;
+    const float our_cost = nodes[node_index].aabb.half_area() * our_count;
+    constexpr int BINS = 8;
+    int best_axis = 0;
+    float best_position = 0;
+    float best_cost = our_cost;
+    for (int axis = 0; axis < 3; axis++) {
+        float min_c = 1e30f, max_c = -1e30f;
+        for (int i = c2; i < c1; i++) {
+            min_c = fmin_(min_c, comp(tris[i].normal, axis));
+            max_c = fmax_(max_c, comp(tris[i].normal, axis));
+        }
+        if (min_c == max_c) continue;
+        float scale = BINS / (max_c - min_c);
+        Aabb bin_box[BINS];
+        int bin_count[BINS] = {0};
+        for (int i = c2; i < c1; i++) {
+            const int b = std::min(BINS - 1, (int)((comp(tris[i].normal, axis) - min_c) * scale));
+            bin_count[b]++;
+            bin_box[b].expand(tris[i]);
+        }
+        float left_area[BINS - 1], right_area[BINS - 1];
+        int left_count[BINS - 1];
+        int left_sum = 0;
+        Aabb left_box, right_box;
+        for (int i = 0; i + 1 < BINS; i++) {
+            left_sum += bin_count[i];
+            left_count[i] = left_sum;
+            left_box.expand(bin_box[i]);
+            left_area[i] = left_box.half_area();
+            right_box.expand(bin_box[BINS - 1 - i]);
+            right_area[BINS - 2 - i] = right_box.half_area();
+        }
+        scale = (max_c - min_c) / BINS;
+        for (int i = 0; i + 1 < BINS; i++) {
+            const float plane_cost = left_count[i] * left_area[i] + (our_count - left_count[i]) * right_area[i];
+            if (plane_cost != 0 && plane_cost < best_cost) {
+                best_axis = axis;
+                best_position = min_c + scale * (i + 1);
+                best_cost = plane_cost;
+            }
+        }
+    }
+    if (best_cost >= our_cost) return;
+    int i = c2, j = c1 - 1;
+    const int sc = (int)s->spheres.size();
+    while (i <= j) {
+        if (comp(tris[i].normal, best_axis) < best_position) {
+            i++;
+        } else {
+            std::swap(tris[i], tris[j]);
+            std::swap(s->material_indices[sc + i], s->material_indices[sc + j]);
+            j--;
+        }
+    }
+    if (i == c1 || i == c2) return;
+    const int left = (int)nodes.size();
+    nodes.emplace_back();
+    const int right = (int)nodes.size();
+    nodes.emplace_back();
+    nodes[left].child2 = c2;
+    nodes[left].child1 = i;
+    nodes[right].child2 = i;
+    nodes[right].child1 = c1;
+    maybe_split(s, left, max_depth - 1);
+    maybe_split(s, right, max_depth - 1);
+    nodes[node_index].child1 = left;
+    nodes[node_index].child2 = right;
+}
+
+// ---------------------------------------------------------------- scene.cu:1002-1036
+void generate_bvh(orc_scene *s, int max_depth) {
+    s->bvh.clear();
+    s->bvh.reserve(std::max<size_t>(1, s->triangles.size() * 2));
+    s->bvh.emplace_back();
+    s->bvh[0].child2 = 0;
+    s->bvh[0].child1 = (int)s->triangles.size();
+    maybe_split(s, 0, max_depth);
+    for (auto &t : s->triangles) {
+        t.p2p1 = t.p2p1 - t.p1;
+        t.p3p1 = t.p3p1 - t.p1;
+        t.normal = normalise(cross(t.p3p1, t.p2p1));
+    }
+}
+
+std::string join_root(const char *root, const std::string &p) {
+    if (!root || !*root || (!p.empty() && p[0] == '/')) return p;
+    std::string r(root);
+    if (r.back() != '/') r += '/';
+    return r + p;
+}
+
+// ---------------------------------------------------------------- scene.cu:491-546
+bool load_ply(std::vector<Triangle> &out, const std::string &path) {
+    std::ifstream f(path, std::ios_base::binary);
+    if (!f) { g_err = "cannot open ply " + path; return false; }
+    std::string line;
+    std::getline(f, line); std::getline(f, line); std::getline(f, line);
+    if (line.size() < 16) { g_err = "bad ply header " + path; return false; }
+    const int vertex_count = std::stoi(line.substr(15));
+    for (int k = 0; k < 9; k++) std::getline(f, line);
+    if (line.size() < 14) { g_err = "bad ply header " + path; return false; }
+    const int face_count = std::stoi(line.substr(13));
+    std::getline(f, line); std::getline(f, line);
+    struct Vertex { V3 position, normal; float u, v; };
+    std::vector<Vertex> verts(vertex_count);
+    f.read(reinterpret_cast<char *>(verts.data()), sizeof(Vertex) * verts.size());
+    std::vector<int32_t> idx;
+    for (int i = 0; i < face_count; i++) {
+        const int n = f.get();
+        if (n < 0) { g_err = "truncated ply " + path; return false; }
+        idx.resize(n);
+        f.read(reinterpret_cast<char *>(idx.data()), sizeof(int32_t) * n);
+        for (int j = 2; j < n; j++) {
+            Triangle t;
+            t.p1 = verts[idx[0]].position;
+            t.p2p1 = verts[idx[j - 1]].position;
+            t.p3p1 = verts[idx[j]].position;
+            t.normal = (1.0f / 3.0f) * (t.p1 + t.p2p1 + t.p3p1);
+            out.push_back(t);
+        }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- scene.cu:548-567
+bool load_pfm(orc_scene *s, const std::string &path) {
+    std::ifstream f(path, std::ios_base::binary);
+    if (!f) { g_err = "cannot open pfm " + path; return false; }
+    std::string line;
+    std::getline(f, line);
+    std::getline(f, line);
+    std::stringstream ss(line);
+    ss >> s->env_w >> s->env_h;
+    std::getline(f, line);
+    s->env.assign((size_t)s->env_w * s->env_h, V3{0, 0, 0});
+    f.read(reinterpret_cast<char *>(s->env.data()), sizeof(V3) * s->env.size());
+    return true;
+}
+
+std::vector<std::string> split_ws(const std::string &s) {
+    std::vector<std::string> out;
+    std::istringstream is(s);
+    for (std::string t; is >> t;) out.push_back(t);
+    return out;
+}
+float num(const std::vector<std::string> &t, size_t i) { return i < t.size() ? std::strtof(t[i].c_str(), nullptr) : 0.0f; }
+int inum(const std::vector<std::string> &t, size_t i) { return i < t.size() ? std::atoi(t[i].c_str()) : 0; }
+
+// ---------------------------------------------------------------- scene.cu:569-831
+orc_scene *load_scene(const char *path, int use_bvh, const char *root, const int32_t *image,
+                      const float *exposure) {
+    auto *s = new orc_scene();
+    std::ifstream file(path);
+    if (!file) { g_err = std::string("cannot open scene ") + path; delete s; return nullptr; }
+    std::unordered_map<std::string, uint16_t> mat_map;
+    std::vector<uint16_t> sphere_mats, tri_mats;
+    bool have_env = false;
+    for (std::string line; std::getline(file, line);) {
+        while (!line.empty() && (line.back() == '\r' || line.back() == '\n')) line.pop_back();
+        if (line.empty()) continue;
+        const size_t sp = line.find(' ');
+        const std::string cmd = line.substr(0, sp);
+        const std::vector<std::string> t = split_ws(line);
+        auto mat_of = [&](const std::string &name, uint16_t *out) {
+            auto it = mat_map.find(name);
+            if (it == mat_map.end()) { g_err = "unknown material " + name; return false; }
+            *out = it->second;
+            return true;
+        };
+        if (cmd == "sky") {
+            s->env.assign(1, V3{num(t, 1), num(t, 2), num(t, 3)});
+            s->env_w = s->env_h = 1;
+            have_env = true;
+        } else if (cmd == "sky_map") {
+            if (t.size() < 2 || !load_pfm(s, join_root(root, t[1]))) { delete s; return nullptr; }
+            have_env = true;
+            std::printf("Loaded environment map with size %d,%d\n", s->env_w, s->env_h);
+        } else if (cmd == "camera") {
+            s->camera_position = {num(t, 2), num(t, 3), num(t, 4)};
+            s->forward = normalise(V3{num(t, 6), num(t, 7), num(t, 8)});
+            s->up = normalise(V3{num(t, 10), num(t, 11), num(t, 12)});
+            s->vertical_fov = (float)(num(t, 14) * (3.14159265358979323846 / 180));
+        } else if (cmd == "material") {
+            if (t.size() < 2) continue;
+            mat_map[t[1]] = (uint16_t)s->materials.size();
+            Material m;
+            m.specular = {1, 1, 1};
+            m.diffuse = {1, 1, 1};
+            m.emitted = {0, 0, 0};
+            m.metallicity = 0;
+            m.roughness = 0;
+            m.ior = 0;
+            for (size_t k = 2; k < t.size(); k++) {
+                if (t[k] == "diffuse") { m.diffuse = {num(t, k + 1), num(t, k + 2), num(t, k + 3)}; k += 3; }
+                else if (t[k] == "specular") { m.specular = {num(t, k + 1), num(t, k + 2), num(t, k + 3)}; k += 3; }
+                else if (t[k] == "emit") { m.emitted = {num(t, k + 1), num(t, k + 2), num(t, k + 3)}; k += 3; }
+                else if (t[k] == "metallicity") { m.metallicity = num(t, ++k); }
+                else if (t[k] == "roughness") { m.roughness = num(t, ++k); }
+                else if (t[k] == "ior") { m.ior = num(t, ++k); }
+            }
+            s->materials.push_back(m);
+        } else if (cmd == "sphere") {
+            uint16_t m;
+            if (t.size() < 2 || !mat_of(t[1], &m)) { delete s; return nullptr; }
+            sphere_mats.push_back(m);
+            s->spheres.push_back(Sphere{{num(t, 2), num(t, 3), num(t, 4)}, num(t, 5)});
+        } else if (cmd == "triangle") {
+            uint16_t m;
+            if (t.size() < 2 || !mat_of(t[1], &m)) { delete s; return nullptr; }
+            tri_mats.push_back(m);
+            Triangle tr;
+            tr.p1 = {num(t, 2), num(t, 3), num(t, 4)};
+            tr.p2p1 = {num(t, 5), num(t, 6), num(t, 7)};
+            tr.p3p1 = {num(t, 8), num(t, 9), num(t, 10)};
+            tr.normal = (1.0f / 3.0f) * (tr.p1 + tr.p2p1 + tr.p3p1);
+            s->triangles.push_back(tr);
+        } else if (cmd == "quad") {
+            uint16_t m;
+            if (t.size() < 2 || !mat_of(t[1], &m)) { delete s; return nullptr; }
+            tri_mats.push_back(m);
+            tri_mats.push_back(m);
+            const V3 p1{num(t, 2), num(t, 3), num(t, 4)}, p2{num(t, 5), num(t, 6), num(t, 7)};
+            const V3 p3{num(t, 8), num(t, 9), num(t, 10)}, p4{num(t, 11), num(t, 12), num(t, 13)};
+            Triangle a{p1, p2, p3, {0, 0, 0}};
+            a.normal = (1.0f / 3.0f) * (a.p1 + a.p2p1 + a.p3p1);
+            s->triangles.push_back(a);
+            Triangle b{p1, p3, p4, {0, 0, 0}};
+            b.normal = (1.0f / 3.0f) * (b.p1 + b.p2p1 + b.p3p1);
+            s->triangles.push_back(b);
+        } else if (cmd == "ply") {
+            uint16_t m;
+            if (t.size() < 3 || !mat_of(t[1], &m)) { delete s; return nullptr; }
+            const size_t before = s->triangles.size();
+            if (!load_ply(s->triangles, join_root(root, t[2]))) { delete s; return nullptr; }
+            for (size_t k = before; k < s->triangles.size(); k++) tri_mats.push_back(m);
+        } else if (cmd == "image") {
+            s->width = inum(t, 1);
+            s->height = inum(t, 2);
+            s->ray_count = inum(t, 3);
+            s->bounces = inum(t, 4);
+            s->exposure = num(t, 5);
+        }
+    }
+    if (image) { s->width = image[0]; s->height = image[1]; s->ray_count = image[2]; s->bounces = image[3]; }
+    if (exposure) s->exposure = *exposure;
+    if (!have_env) { s->env.assign(1, V3{0, 0, 0}); s->env_w = s->env_h = 1; }  // reference: UB
+    s->material_indices = sphere_mats;
+    s->material_indices.insert(s->material_indices.end(), tri_mats.begin(), tri_mats.end());
+    precompute_camera_data(s);
+    generate_bvh(s, use_bvh ? 30 : 0);
+    s->min_coord = s->bvh[0].aabb.mn;
+    V3 mx = s->bvh[0].aabb.mx;
+    for (const auto &sp : s->spheres) {
+        const V3 r{sp.radius, sp.radius, sp.radius};
+        mx = vmax(mx, sp.center + r);
+        s->min_coord = vmin(s->min_coord, sp.center - r);
+    }
+    s->inv_dimensions = {1 / mx.x, 1 / mx.y, 1 / mx.z};
+    return s;
+}
+
+// ---------------------------------------------------------------- scene.cu:44-60 (key)
+uint16_t sat_u16(double v) {
+    if (!(v > 0.0)) return 0;           // NaN, <= 0
+    if (v >= 65535.0) return 65535;
+    return (uint16_t)v;
+}
+uint16_t interleave_5(uint16_t x) {     // scene.cu:44-51, including the 0x1000010100011 literal
+    x = (uint16_t)((x | (x << 8)) & 0b1000000001111);
+    x = (uint16_t)((x | (x << 4)) & 0x1000010100011LL);
+    x = (uint16_t)((x | (x << 2)) & 0b1001001001001);
+    return x;
+}
+uint16_t morton_code(V3 v) {            // scene.cu:53-60
+    const uint16_t x = sat_u16((double)v.x * 31.99);
+    const uint16_t y = sat_u16((double)v.y * 31.99);
+    const uint16_t z = sat_u16((double)v.z * 31.99);
+    return (uint16_t)(interleave_5(x) | (interleave_5(y) << 1) | (interleave_5(z) << 2));
+}
+
+// float(t) < 0.005 as double  <=>  t < 0x1.47ae16p-8f (smallest float whose double >= 0.005).
+inline bool below_eps(float t) { return (double)t < 0.005; }
+
+// ---------------------------------------------------------------- scene.cu:109-132
+inline bool ray_aabb(const Aabb &b, V3 o, V3 n_inv, float &tmin, float tmax) {
+    tmin = 0.0f;
+    float t1 = (b.mn.x - o.x) * n_inv.x, t2 = (b.mx.x - o.x) * n_inv.x;
+    tmin = fmin_(fmax_(t1, tmin), fmax_(t2, tmin));
+    tmax = fmax_(fmin_(t1, tmax), fmin_(t2, tmax));
+    t1 = (b.mn.y - o.y) * n_inv.y; t2 = (b.mx.y - o.y) * n_inv.y;
+    tmin = fmin_(fmax_(t1, tmin), fmax_(t2, tmin));
+    tmax = fmax_(fmin_(t1, tmax), fmin_(t2, tmax));
+    t1 = (b.mn.z - o.z) * n_inv.z; t2 = (b.mx.z - o.z) * n_inv.z;
+    tmin = fmin_(fmax_(t1, tmin), fmax_(t2, tmin));
+    tmax = fmax_(fmin_(t1, tmax), fmin_(t2, tmax));
+    return tmin <= tmax;
+}
+
+// Möller–Trumbore body, scene.cu:162-195. Returns true and t when accepted against `closest`.
+inline bool ray_tri(const Triangle &tr, V3 o, V3 d, float closest, float *t_out) {
+    const V3 h = cross(d, tr.p3p1);
+    const float a = dot(h, tr.p2p1);
+    if (a == 0) return false;
+    const float f = 1 / a;
+    const V3 s = o - tr.p1;
+    const float u = dot(s, h) * f;
+    if (u < 0 || u > 1) return false;
+    const V3 q = cross(s, tr.p2p1);
+    const float v = dot(d, q) * f;
+    if (v < 0 || u + v > 1) return false;
+    const float t = dot(tr.p3p1, q) * f;
+    if (below_eps(t) || t >= closest) return false;
+    *t_out = t;
+    return true;
+}
+
+// Sphere body, scene.cu:340-371. Returns 1 if accepted (t_out set).
+inline bool ray_sphere(const Sphere &sp, V3 o, V3 d, float closest, float *t_out) {
+    const V3 off = sp.center - o;
+    const float mhb = dot(off, d);
+    const float qc = magsq(off) - sp.radius * sp.radius;
+    const float qd = mhb * mhb - qc;
+    if (qd < 0) return false;
+    const float hs = sqrtf(qd);
+    float t = mhb - hs;
+    if (t < closest && !below_eps(t)) { *t_out = t; return true; }
+    t = mhb + hs;
+    if (t < closest && !below_eps(t)) { *t_out = t; return true; }
+    return false;
+}
+
+struct Counters {
+    uint64_t pn = 0, iv = 0, tt = 0, st = 0, ht = 0, hs = 0, miss = 0, live = 0, dead = 0;
+    uint32_t max_stack = 0;
+    void add(const Counters &o) {
+        pn += o.pn; iv += o.iv; tt += o.tt; st += o.st; ht += o.ht; hs += o.hs; miss += o.miss;
+        live += o.live; dead += o.dead; max_stack = std::max(max_stack, o.max_stack);
+    }
+};
+
+// ---------------------------------------------------------------- scene.cu:134-241
+void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index, Counters &c) {
+    const V3 n_inv{1 / d.x, 1 / d.y, 1 / d.z};
+    uint32_t idx_stack[31];
+    float dist_stack[31];
+    int sc = 1;
+    idx_stack[0] = 0;
+    dist_stack[0] = 0;
+    const int sphere_count = (int)s->spheres.size();
+    while (sc) {
+        sc--;
+        const float dist = dist_stack[sc];
+        if (dist >= closest) continue;
+        const BvhNode &node = s->bvh[idx_stack[sc]];
+        c.pn++;
+        if (is_leaf(node)) {
+            for (int i = node.child2; i < node.child1; i++) {
+                c.tt++;
+                float t;
+                if (ray_tri(s->triangles[i], o, d, closest, &t)) {
+                    closest = t;
+                    index = sphere_count + i;
+                }
+            }
+        } else {
+            c.iv++;
+            float d1, d2;
+            const bool h1 = ray_aabb(s->bvh[node.child1].aabb, o, n_inv, d1, closest);
+            const bool h2 = ray_aabb(s->bvh[node.child2].aabb, o, n_inv, d2, closest);
+            if (h1 && h2) {
+                if (d1 < d2) {
+                    idx_stack[sc] = node.child1; dist_stack[sc] = d1; sc++;
+                    idx_stack[sc] = node.child2; dist_stack[sc] = d2; sc++;
+                } else {
+                    idx_stack[sc] = node.child2; dist_stack[sc] = d2; sc++;
+                    idx_stack[sc] = node.child1; dist_stack[sc] = d1; sc++;
+                }
+            } else if (h1) {
+                idx_stack[sc] = node.child1; dist_stack[sc] = d1; sc++;
+            } else if (h2) {
+                idx_stack[sc] = node.child2; dist_stack[sc] = d2; sc++;
+            }
+            if ((uint32_t)sc > c.max_stack) c.max_stack = (uint32_t)sc;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- scene.cu:284-318
+V3 equal_area_project(V3 dir) {
+    const float x = std::fabs(dir.x), y = std::fabs(dir.y), z = std::fabs(dir.z);
+    const float r = sqrtf(1 - fmin_(z, 1.0f));
+    const float a = fmax_(x, y);
+    float b = fmin_(x, y);
+    b = a == 0 ? 0 : b / a;
+    float phi = (float)((2 / 3.14159265358979323846) * (double)rt_atan01(b));
+    if (x < y) phi = 1 - phi;
+    float v = phi * r;
+    float u = r - v;
+    if (dir.z < 0) {
+        const float old_v = v;
+        v = 1 - u;
+        u = 1 - old_v;
+    }
+    u = std::copysign(u, dir.x);
+    v = std::copysign(v, dir.y);
+    return {(u + 1) * 0.5f, (v + 1) * 0.5f, 0};
+}
+
+int env_texel(const orc_scene *s, V3 d) {                  // scene.cu:380-391
+    const float dx = (float)((double)d.x * -0.386527 + (double)d.z * 0.922278);
+    const float dy = (float)((double)d.x * -0.922278 + (double)d.z * -0.386527);
+    const float dz = d.y;
+    const V3 uv = equal_area_project({dx, dy, dz});
+    const int tx = (int)((double)(clamp01(uv.x) * (s->env_w - 1)) + 0.5);
+    const int ty = (int)((double)(clamp01(uv.y) * (s->env_h - 1)) + 0.5);
+    return ty * s->env_h + tx;
+}
+
+// ---------------------------------------------------------------- scene.cu:320-487
+// gpu: key-based early-out and key write (the __CUDA_ARCH__ branches); else CPU branches.
+void process_ray(const orc_scene *s, RayData *rp, uint32_t *key, Rng rng, bool gpu, Counters &c) {
+    if (gpu) {
+        if (*key == 0xFFFFFFFFu) { c.dead++; return; }
+    } else if (is_black(rp->transmitted)) {
+        c.dead++;
+        return;
+    }
+    c.live++;
+    RayData rd = *rp;
+    float closest = 1e30f;
+    int index = -1;
+    const V3 o = rd.origin, d = rd.dir;
+    const int sphere_count = (int)s->spheres.size();
+    for (int i = 0; i < sphere_count; i++) {
+        c.st++;
+        float t;
+        if (ray_sphere(s->spheres[i], o, d, closest, &t)) { closest = t; index = i; }
+    }
+    bvh_closest_hit(s, o, d, closest, index, c);
+    if (index == -1) {
+        c.miss++;
+        const V3 sky = s->env[env_texel(s, d)];
+        rd.collected = rd.collected + sky * rd.transmitted;
+        rd.transmitted = {0, 0, 0};
+    } else {
+        const V3 hit = o + closest * d;
+        rd.origin = hit;
+        V3 normal;
+        if (index < sphere_count) {
+            c.hs++;
+            const Sphere &sp = s->spheres[index];
+            normal = (1 / sp.radius) * (hit - sp.center);
+        } else {
+            c.ht++;
+            normal = s->triangles[index - sphere_count].normal;
+        }
+        const Material &m = s->materials[s->material_indices[index]];
+        rd.collected = rd.collected + m.emitted * rd.transmitted;
+        const bool front = dot(normal, d) < 0;
+        if (!front) normal = -normal;
+        const V3 rough = normalise(normal + m.roughness * random_on_sphere(&rng));
+        const float cos_theta = dot(rough, d);
+        if (m.ior == 0) {
+            if (random01(&rng) <= m.metallicity) {
+                rd.transmitted = rd.transmitted * m.specular;
+                rd.dir = d - (2 * cos_theta) * rough;
+            } else {
+                rd.transmitted = rd.transmitted * m.diffuse;
+                rd.dir = normalise(normal + random_on_sphere(&rng));
+            }
+        } else {
+            float ior = m.ior;
+            float inv_ior = 1 / ior;
+            if (front) std::swap(ior, inv_ior);
+            const float sin2 = 1 - cos_theta * cos_theta;
+            float r0 = (1 - ior) / (1 + ior);
+            r0 *= r0;
+            const float cs = 1 + cos_theta;
+            const float refl = r0 + (1 - r0) * cs * cs * cs * cs * cs;
+            if (sin2 > inv_ior * inv_ior || random01(&rng) < refl) {
+                rd.transmitted = rd.transmitted * m.specular;
+                rd.dir = d - (2 * cos_theta) * rough;
+            } else {
+                rd.transmitted = rd.transmitted * m.diffuse;
+                const V3 perp = ior * (d - cos_theta * rough);
+                const V3 par = (-sqrtf(1 - magsq(perp))) * rough;
+                rd.dir = normalise(par + perp);
+            }
+        }
+    }
+    if (gpu) {
+        if (is_black(rd.transmitted)) {
+            *key = 0xFFFFFFFFu;
+        } else {
+            *key = ((uint32_t)morton_code((rd.origin - s->min_coord) * s->inv_dimensions) << 16) |
+                   (uint32_t)morton_code(0.5f * (rd.dir + V3{1, 1, 1}));
+        }
+    }
+    *rp = rd;
+}
+
+// ---------------------------------------------------------------- scene.cu:78-105
+void generate_ray(const orc_scene *s, RayData *rays, uint32_t *idx, uint32_t *keys, int rtc, int i, int seed) {
+    Rng rng;
+    xor_srand(&rng, (uint32_t)i * 0x85810BEAu + 709579u * (uint32_t)seed);
+    const int fb = i / rtc;
+    const int x = fb % s->width, y = fb / s->width;
+    if (y < s->height) {
+        if (idx) { idx[i] = (uint32_t)i; keys[i] = 0; }
+        const float xc = (x + random01(&rng)) * s->inv_width;
+        const float yc = (y + random01(&rng)) * s->inv_height;
+        RayData r;
+        r.origin = s->camera_position;
+        r.dir = normalise(s->near_plane_top_left + xc * s->scaled_right - yc * s->scaled_up);
+        r.transmitted = {1, 1, 1};
+        r.collected = {0, 0, 0};
+        rays[i] = r;
+    }
+}
+
+int nthreads(int t) {
+#ifdef _OPENMP
+    return t > 0 ? t : omp_get_max_threads();
+#else
+    (void)t;
+    return 1;
+#endif
+}
+
+// Pass p of the reference's `while (remaining_rays)` loop (raytracing.cu:222-227).
+void pass_params(const orc_scene *s, int p, int *rtc, int *remaining_after) {
+    const int before = s->ray_count - 20 * p;
+    *rtc = std::min(before, 20);
+    *remaining_after = before - *rtc;
+}
+int pass_total(const orc_scene *s) { return (s->ray_count + 19) / 20; }
+
+// One GPU-semantics pass: generate, bounces (process + stable sort), per-pixel ordered sum.
+void gpu_pass(const orc_scene *s, int p, bool sort, float *pass_sum, Counters &total, uint64_t *hist,
+              uint64_t *sorted, int threads) {
+    int rtc, rem;
+    pass_params(s, p, &rtc, &rem);
+    const int64_t n = (int64_t)rtc * s->width * s->height;
+    std::vector<RayData> rays(n);
+    std::vector<uint32_t> idx(n), keys(n), idx2, keys2;
+    const int nt = nthreads(threads);
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int64_t i = 0; i < n; i++) generate_ray(s, rays.data(), idx.data(), keys.data(), rtc, (int)i, rem);
+    for (int b = 0; b < s->bounces; b++) {
+        const uint32_t seed = (uint32_t)(rem * 20 + b);
+        std::vector<Counters> per(nt);
+#pragma omp parallel num_threads(nt)
+        {
+#ifdef _OPENMP
+            Counters &c = per[omp_get_thread_num()];
+#else
+            Counters &c = per[0];
+#endif
+#pragma omp for schedule(dynamic, 4096)
+            for (int64_t slot = 0; slot < n; slot++) {   // raytracing.cu:83-94
+                Rng rng;
+                xor_srand(&rng, (uint32_t)slot * 4137874753u + 279220567u * seed);
+                process_ray(s, &rays[idx[slot]], &keys[slot], rng, true, c);
+            }
+        }
+        for (auto &c : per) total.add(c);
+        if (hist) {
+            uint64_t *h = hist + (size_t)b * 65;
+            for (int64_t k = 0; k < n; k++) h[orc_key_bucket(keys[k])]++;
+        }
+        if (sort && b + 1 != s->bounces) {              // raytracing.cu:238-247: stable sort pairs
+            std::vector<uint32_t> order(n);
+            for (int64_t k = 0; k < n; k++) order[k] = (uint32_t)k;
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t c) { return keys[a] < keys[c]; });
+            idx2.resize(n);
+            keys2.resize(n);
+            for (int64_t k = 0; k < n; k++) { idx2[k] = idx[order[k]]; keys2[k] = keys[order[k]]; }
+            idx.swap(idx2);
+            keys.swap(keys2);
+            *sorted += (uint64_t)n;
+        }
+    }
+    const int64_t pixels = (int64_t)s->width * s->height;
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int64_t px = 0; px < pixels; px++) {
+        V3 sum{0, 0, 0};
+        for (int k = 0; k < rtc; k++) sum = sum + rays[px * rtc + k].collected;
+        pass_sum[px * 3 + 0] = sum.x;
+        pass_sum[px * 3 + 1] = sum.y;
+        pass_sum[px * 3 + 2] = sum.z;
+    }
+    total.live += 0;
+    (void)n;
+}
+
+}  // namespace
+
+// ==================================================================== C API
+extern "C" {
+
+const char *orc_last_error(void) { return g_err.c_str(); }
+
+orc_scene *orc_load_scene(const char *path, int use_bvh, const char *asset_root, const int32_t *image,
+                          const float *exposure) {
+    try {
+        return load_scene(path, use_bvh, asset_root, image, exposure);
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+void orc_free_scene(orc_scene *s) { delete s; }
+
+void orc_get_info(const orc_scene *s, orc_info *o) {
+    o->width = s->width; o->height = s->height; o->ray_count = s->ray_count; o->bounces = s->bounces;
+    o->exposure = s->exposure;
+    o->sphere_count = (int32_t)s->spheres.size();
+    o->triangle_count = (int32_t)s->triangles.size();
+    o->material_count = (int32_t)s->materials.size();
+    o->bvh_node_count = (int32_t)s->bvh.size();
+    o->env_width = s->env_w; o->env_height = s->env_h;
+}
+
+int orc_camera_floats(void) { return 29; }
+
+void orc_get_arrays(const orc_scene *s, void *spheres, void *triangles, uint16_t *mi, void *materials,
+                    void *bvh, float *env, float *cam) {
+    if (spheres && !s->spheres.empty()) std::memcpy(spheres, s->spheres.data(), s->spheres.size() * 16);
+    if (triangles && !s->triangles.empty()) std::memcpy(triangles, s->triangles.data(), s->triangles.size() * 48);
+    if (mi && !s->material_indices.empty()) std::memcpy(mi, s->material_indices.data(), s->material_indices.size() * 2);
+    if (materials && !s->materials.empty()) std::memcpy(materials, s->materials.data(), s->materials.size() * 48);
+    if (bvh) std::memcpy(bvh, s->bvh.data(), s->bvh.size() * 32);
+    if (env) std::memcpy(env, s->env.data(), s->env.size() * 12);
+    if (cam) {
+        const V3 v[] = {s->camera_position, s->forward, s->up};
+        int k = 0;
+        for (const V3 &x : v) { cam[k++] = x.x; cam[k++] = x.y; cam[k++] = x.z; }
+        cam[k++] = s->vertical_fov;
+        const V3 w[] = {s->min_coord, s->inv_dimensions, s->scaled_right, s->scaled_up, s->near_plane_top_left};
+        for (const V3 &x : w) { cam[k++] = x.x; cam[k++] = x.y; cam[k++] = x.z; }
+        cam[k++] = s->inv_width;
+        cam[k++] = s->inv_height;
+        cam[k++] = s->exposure;
+    }
+}
+
+int orc_render_gpu_semantics(const orc_scene *s, int sort, int pass_begin, int pass_count, float *fb,
+                             orc_stats *stats, uint64_t *bucket_hist, int threads) {
+    const int P = pass_total(s);
+    if (pass_count < 0) pass_count = P - pass_begin;
+    if (pass_begin < 0 || pass_begin + pass_count > P) { g_err = "pass range"; return -1; }
+    const int64_t pixels = (int64_t)s->width * s->height;
+    std::vector<float> sum(pixels * 3);
+    Counters total;
+    uint64_t sorted = 0, generated = 0;
+    for (int p = pass_begin; p < pass_begin + pass_count; p++) {
+        uint64_t *h = bucket_hist ? bucket_hist + (size_t)(p - pass_begin) * s->bounces * 65 : nullptr;
+        gpu_pass(s, p, sort != 0, sum.data(), total, h, &sorted, threads);
+        int rtc, rem;
+        pass_params(s, p, &rtc, &rem);
+        generated += (uint64_t)rtc * pixels;
+        for (int64_t k = 0; k < pixels * 3; k++) fb[k] = fb[k] + sum[k];
+    }
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->generated_rays = generated;
+        stats->live_segments = total.live;
+        stats->dead_slots = total.dead;
+        stats->nodes_popped = total.pn;
+        stats->internal_visits = total.iv;
+        stats->triangle_tests = total.tt;
+        stats->sphere_tests = total.st;
+        stats->hits_triangle = total.ht;
+        stats->hits_sphere = total.hs;
+        stats->misses = total.miss;
+        stats->sorted_items = sorted;
+        stats->max_stack = total.max_stack;
+        stats->passes = (uint32_t)pass_count;
+    }
+    return 0;
+}
+
+int orc_render_pass_sums(const orc_scene *s, int sort, int pass_begin, int pass_count, float *out, int threads) {
+    const int P = pass_total(s);
+    if (pass_count < 0) pass_count = P - pass_begin;
+    if (pass_begin < 0 || pass_begin + pass_count > P) { g_err = "pass range"; return -1; }
+    const int64_t pixels = (int64_t)s->width * s->height;
+    Counters total;
+    uint64_t sorted = 0;
+    for (int p = pass_begin; p < pass_begin + pass_count; p++)
+        gpu_pass(s, p, sort != 0, out + (size_t)(p - pass_begin) * pixels * 3, total, nullptr, &sorted, threads);
+    return 0;
+}
+
+// raytracing.cu:122-163 (timed span = "CPU Took").  The inner loop's `i` shadows the bounce index,
+// so the seed does not depend on the bounce (raytracing.cu:142-149).
+int orc_render_cpu_path(const orc_scene *s, float *fb, int pass_limit, int threads, double *seconds) {
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    const int nt = nthreads(threads);
+    const int64_t pixels = (int64_t)s->width * s->height;
+    std::vector<RayData> rays((size_t)pixels * 20);
+    std::memset(fb, 0, sizeof(float) * pixels * 3);
+    int remaining = s->ray_count;
+    int passes = 0;
+    Counters dummy;
+    while (remaining && (pass_limit < 0 || passes < pass_limit)) {
+        const int rtc = std::min(remaining, 20);
+        remaining -= rtc;
+        const int total = rtc * s->width * s->height;
+#pragma omp parallel for schedule(dynamic, 1000) num_threads(nt)
+        for (int i = 0; i < total; i++) generate_ray(s, rays.data(), nullptr, nullptr, rtc, i, remaining);
+        for (int b = 0; b < s->bounces; b++) {
+#pragma omp parallel for schedule(dynamic, 1000) num_threads(nt)
+            for (int i = 0; i < total; i++) {
+                Rng rng;
+                xor_srand(&rng, 1905678123u * (uint32_t)i + 345903u * (uint32_t)(remaining * 20 + i));
+                Counters c;
+                process_ray(s, &rays[i], nullptr, rng, false, c);
+            }
+        }
+        for (int i = 0; i < total; i++) {                    // raytracing.cu:114-120
+            float *p = fb + (size_t)(i / rtc) * 3;
+            p[0] = p[0] + rays[i].collected.x;
+            p[1] = p[1] + rays[i].collected.y;
+            p[2] = p[2] + rays[i].collected.z;
+        }
+        passes++;
+    }
+    (void)dummy;
+    const auto t1 = std::chrono::high_resolution_clock::now();
+    if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+    return passes;
+}
+
+// raytracing.cu:21-74 with the launch parameters of :376-382.
+void orc_bloom(float *fb, int w, int h, float threshold, int radius) {
+    const int64_t n = (int64_t)w * h;
+    std::vector<V3> img(n), bright(n), blur(n);
+    std::memcpy(img.data(), fb, sizeof(V3) * n);
+    for (int64_t i = 0; i < n; i++) {
+        const float lum = dot(img[i], V3{0.2126f, 0.7152f, 0.0722f});
+        bright[i] = lum > threshold ? img[i] : V3{0, 0, 0};
+    }
+    for (int64_t i = 0; i < n; i++) {
+        const int x = (int)(i % w), y = (int)(i / w);
+        V3 sum{0, 0, 0};
+        int count = 0;
+        for (int dx = -radius; dx <= radius; dx++) {
+            const int nx = x + dx;
+            if (nx >= 0 && nx < w) { sum = sum + bright[(int64_t)y * w + nx]; count++; }
+        }
+        blur[i] = (1.0f / count) * sum;
+    }
+    for (int64_t i = 0; i < n; i++) {
+        const int x = (int)(i % w), y = (int)(i / w);
+        V3 sum{0, 0, 0};
+        int count = 0;
+        for (int dy = -radius; dy <= radius; dy++) {
+            const int ny = y + dy;
+            if (ny >= 0 && ny < h) { sum = sum + blur[(int64_t)ny * w + x]; count++; }
+        }
+        bright[i] = (1.0f / count) * sum;
+    }
+    for (int64_t i = 0; i < n; i++) img[i] = img[i] + bright[i];
+    std::memcpy(fb, img.data(), sizeof(V3) * n);
+}
+
+// raytracing.cu:286-303
+void orc_tonemap(const float *fb, int w, int h, float exposure, int ray_count, uint8_t *out) {
+    const float scale = exposure / ray_count;
+    for (int64_t i = 0; i < (int64_t)w * h * 3; i++) {
+        const float p = scale * fb[i];
+        const float v = sqrtf(p / (p + 1)) * 255.999f;
+        out[i] = (v == v && v > 0) ? (uint8_t)(int)v : 0;
+    }
+}
+
+void orc_pcg_stream(uint32_t seed, int n, uint32_t *out) {
+    Rng r;
+    xor_srand(&r, seed);
+    for (int i = 0; i < n; i++) out[i] = xor_rand(&r);
+}
+void orc_random_draws(uint32_t seed, int n, float *r01, float *r02, float *rad) {
+    Rng a, b, c;
+    xor_srand(&a, seed); xor_srand(&b, seed); xor_srand(&c, seed);
+    for (int i = 0; i < n; i++) { r01[i] = random01(&a); r02[i] = random02(&b); rad[i] = random_radians(&c); }
+}
+void orc_random_on_sphere(uint32_t seed, int n, float *out) {
+    Rng r;
+    xor_srand(&r, seed);
+    for (int i = 0; i < n; i++) {
+        const V3 v = random_on_sphere(&r);
+        out[3 * i] = v.x; out[3 * i + 1] = v.y; out[3 * i + 2] = v.z;
+    }
+}
+void orc_sincos(const float *x, int n, float *s, float *c) {
+    for (int i = 0; i < n; i++) rt_sincos(x[i], &s[i], &c[i]);
+}
+float orc_atan01(float x) { return rt_atan01(x); }
+uint32_t orc_generate_seed(int32_t i, int32_t seed) { return (uint32_t)i * 0x85810BEAu + 709579u * (uint32_t)seed; }
+uint32_t orc_process_seed(int32_t slot, int32_t seed) { return (uint32_t)slot * 4137874753u + 279220567u * (uint32_t)seed; }
+uint32_t orc_cpu_seed(int32_t i, int32_t rem) { return 1905678123u * (uint32_t)i + 345903u * (uint32_t)(rem * 20 + i); }
+uint16_t orc_interleave_5(uint16_t x) { return interleave_5(x); }
+uint32_t orc_morton(float x, float y, float z) { return morton_code(V3{x, y, z}); }
+int orc_key_bucket(uint32_t key) {
+    if (key == 0xFFFFFFFFu) return 64;
+    const uint32_t mo = key >> 16, md = key & 0xFFFF;
+    const uint32_t qo = (mo & 1) | (((mo >> 1) & 1) << 1) | (((mo >> 2) & 1) << 2);
+    const uint32_t qd = (md & 1) | (((md >> 1) & 1) << 1) | (((md >> 2) & 1) << 2);
+    return (int)((qo << 3) | qd);
+}
+int orc_ray_aabb(const float *bmin, const float *bmax, const float *o, const float *d, float tmax, float *tmin) {
+    Aabb b;
+    b.mn = {bmin[0], bmin[1], bmin[2]};
+    b.mx = {bmax[0], bmax[1], bmax[2]};
+    const V3 n_inv{1 / d[0], 1 / d[1], 1 / d[2]};
+    return ray_aabb(b, V3{o[0], o[1], o[2]}, n_inv, *tmin, tmax) ? 1 : 0;
+}
+int orc_ray_triangle(const float *t12, const float *o, const float *d, float closest, float *t) {
+    Triangle tr;
+    std::memcpy(&tr, t12, 48);
+    return ray_tri(tr, V3{o[0], o[1], o[2]}, V3{d[0], d[1], d[2]}, closest, t) ? 1 : 0;
+}
+int orc_ray_sphere(const float *s4, const float *o, const float *d, float closest, float *t) {
+    Sphere sp{{s4[0], s4[1], s4[2]}, s4[3]};
+    return ray_sphere(sp, V3{o[0], o[1], o[2]}, V3{d[0], d[1], d[2]}, closest, t) ? 1 : 0;
+}
+void orc_env_project(const float *dir, float *uv) {
+    const V3 r = equal_area_project(V3{dir[0], dir[1], dir[2]});
+    uv[0] = r.x; uv[1] = r.y;
+}
+int orc_env_texel(const float *dir, int w, int h) {
+    orc_scene s;
+    s.env_w = w; s.env_h = h;
+    return env_texel(&s, V3{dir[0], dir[1], dir[2]});
+}
+
+}  // extern "C"
