@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X path tracer (BASELINE.json metric: Mrays/s per scene at 1/2/4/8 GPUs).
+
+Workload (default): teapot.scene at 1920x1080, 2048 spp, 16 bounces, sort on (BASELINE.json
+configs[3], the config the north star's roofline target is stated on).  A step is one 20-spp
+pass of the hot path on every GPU: ray generation, 16 x (BVH traversal + shading + reorder
+key, stable reorder), ordered accumulation.  Multi-GPU runs shard whole passes round-robin
+over ranks (rank r renders pass r + N*k); each step ends with an RCCL gather of the per-pass
+framebuffers to rank 0, which adds them in pass order (bit-identical to 1 GPU).  Per-GPU work
+is fixed, so scaling is weak.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scene teapot] [--no-sort]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  `value` = live ray segments (process_ray calls on live slots)
+per second over all GPUs, inputs resident in HBM.  `roofline` prices the dominant kernel
+(process_kernel) with SURVEY.md §8(d)'s logical byte model; `cpu_baseline` times the
+oracle's restatement of the reference `cpu` path on a bounded sample on the host cores.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "cuda-raytracer_amd"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+import numpy as np  # noqa: E402
+
+import rtamd  # noqa: E402
+
+CONFIGS = {
+    # name: (scene file, W, H, spp, bounces, sort, use_bvh)
+    "teapot": ("teapot.scene", 1920, 1080, 2048, 16, True, True),
+    "cornell_plus": ("cornell_plus.scene", 512, 512, 256, 8, True, True),
+    "spheres": ("spheres.scene", 1024, 1024, 1024, 8, True, False),
+    "lamp": ("lamp_available.scene", 1920, 1080, 4096, 32, True, True),
+    "cornell": ("cornell.scene", 256, 256, 64, 4, True, True),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def segment_bytes(st, spheres):
+    """SURVEY.md §8(d) logical bytes of the process kernel, summed over the counted launches."""
+    live = st["live_segments"]
+    hits, hs = st["hits"], st["hits_sphere"]
+    b = live * (8 + 48 + 48 + 4 + 16 * spheres)
+    b += 32 * st["nodes_popped"] + 64 * st["internal_visits"] + 48 * st["triangle_tests"]
+    b += hits * (2 + 48) + (hits - hs) * 48 + hs * 16 + st["misses"] * 12
+    # §8(d) also charges 8 B per terminated slot; this kernel never touches those slots when the
+    # reorder is on (it walks only the live prefix), and reads a 1-B bucket per slot when off.
+    b += st.get("dead_slot_bytes", 0)
+    return b
+
+
+def load_pmc(workload):
+    """HBM traffic per process_kernel launch from the committed rocprofv3 PMC summary."""
+    path = os.path.join(REPO, "profiles", "pmc_process_kernel.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(cfg, args):
+    """Times the oracle's restatement of cpu_raytrace (raytracing.cu:122-163) on a bounded
+    sample of the same scene: full resolution, `--cpu-spp` rays/pixel, same bounces."""
+    exe = os.path.join(REPO, "oracle", "build", "cpu_baseline")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    scene, w, h, _, bounces = cfg[:5]
+    cmd = [exe, os.path.join(rtamd.ASSETS, scene), rtamd.ASSETS, str(w), str(h), str(args.cpu_spp),
+           str(bounces), "1", str(threads)]
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, env=env).stdout
+    rec = json.loads(out.strip().splitlines()[-1])
+    return {
+        "value": round(rec["live_segments"] / rec["seconds"] / 1e6, 3),
+        "unit": "Mrays/s",
+        "cores": rec["threads"],
+        "kind": "port",
+        "sample": "%s %dx%d, %d spp (one pass), %d bounces: %d live segments in %.2f s "
+                  "(oracle cpu_raytrace restatement, -O3 -ffast-math -fopenmp)" % (
+                      scene, w, h, args.cpu_spp, bounces, rec["live_segments"], rec["seconds"]),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="teapot", choices=sorted(CONFIGS))
+    ap.add_argument("--no-sort", action="store_true")
+    ap.add_argument("--cpu-spp", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-counters", action="store_true", help="skip the byte-model counting rerun")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    torch = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = CONFIGS[args.scene]
+    scene_file, W, H, spp, bounces, sort, use_bvh = cfg
+    if args.no_sort:
+        sort = False
+    import make_envmap
+    make_envmap.ensure_envmap(os.path.join(REPO, "assets", "teapot", "textures", "envmap.pfm"))
+    t_load = time.perf_counter()
+    scene = rtamd.Scene(os.path.join(rtamd.ASSETS, scene_file), use_bvh=use_bvh, image=(W, H, spp, bounces))
+    load_s = time.perf_counter() - t_load
+    P = scene.passes
+    ren = rtamd.Renderer(scene, sort=sort, device=local)
+
+    px3 = W * H * 3
+    pass_buf = gather = fb_acc = None
+    if world > 1:
+        pass_buf = torch.empty(px3, dtype=torch.float32, device="cuda")
+        if rank == 0:
+            gather = [torch.empty(px3, dtype=torch.float32, device="cuda") for _ in range(world)]
+            fb_acc = torch.zeros(px3, dtype=torch.float32, device="cuda")
+
+    def barrier_sync():
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    def pass_of(step):
+        return (rank + world * step) % P
+
+    def one_step(step, stats):
+        st = ren.run(pass_begin=pass_of(step), count=1,
+                     d_pass_sums=pass_buf.data_ptr() if pass_buf is not None else None)
+        for k in ("live_segments", "generated_rays"):
+            stats[k] = stats.get(k, 0) + st[k]
+        stats["process_ms"] = stats.get("process_ms", 0.0) + st["process_ms"]
+        stats["sort_ms"] = stats.get("sort_ms", 0.0) + st["sort_ms"]
+        stats["kernel_ms"] = stats.get("kernel_ms", 0.0) + st["kernel_ms"]
+        if world > 1:
+            # RCCL gather of every rank's pass framebuffer; rank 0 adds them in pass order.
+            dist.gather(pass_buf, gather_list=gather, dst=0)
+            if rank == 0:
+                for g in gather:
+                    fb_acc.add_(g)
+
+    warm = {}
+    for s in range(args.warmup):
+        one_step(s, warm)
+    barrier_sync()
+    timed = {}
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        one_step(args.warmup + s, timed)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+
+    live = timed.get("live_segments", 0)
+    proc_ms = timed.get("process_ms", 0.0)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        t = torch.tensor([live], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        live = int(t.item())
+
+    # Byte model: recount the timed passes with the counting kernel variant (untimed).
+    counted = None
+    if not args.no_counters and args.steps > 0:
+        ren.set_counters(True)
+        counted = {}
+        for s in range(args.steps):
+            st = ren.run(pass_begin=pass_of(args.warmup + s), count=1)
+            for k, v in st.items():
+                if isinstance(v, int):
+                    counted[k] = counted.get(k, 0) + v
+        counted["dead_slot_bytes"] = 0 if sort else counted["dead_slots"]
+        ren.set_counters(False)
+
+    if rank == 0:
+        workload = "%s %dx%d %dspp %d bounces sort=%s" % (scene_file, W, H, spp, bounces, "on" if sort else "off")
+        launches = args.steps * bounces
+        ms_launch = proc_ms / launches if launches else 0.0
+        roof = None
+        if counted:
+            bytes_total = segment_bytes(counted, scene.view.sphere_count)
+            bytes_launch = bytes_total / launches
+            achieved = bytes_launch / (ms_launch / 1e3) / 1e9 if ms_launch > 0 else 0.0
+            traffic = load_pmc(workload)
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "process_kernel", "bytes_per_launch": int(bytes_launch),
+                    "ms_per_launch": round(ms_launch, 4),
+                    "model": "SURVEY.md 8(d): per live segment 108+16S + 32*Pn + 64*Iv + 48*Tt + hit(98|66)/miss(12); "
+                             "dead slots: 0 B with sort (never visited), 1 B without; counts from the device "
+                             "counters of the same passes"}
+        value = live / elapsed / 1e6 if elapsed > 0 else 0.0
+        nominal = world * args.steps * 20 * W * H * bounces / elapsed / 1e6 if elapsed > 0 else 0.0
+        ms_step = elapsed / args.steps * 1e3 if args.steps else 0.0
+        out = {
+            "metric": "Mrays/s (live ray segments/s, %s)" % args.scene,
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference scene + assets, procedural stand-in env map (assets missing upstream)",
+            "config": {
+                "workload": workload,
+                "step": "one 20-spp pass (%d rays x %d bounces) per GPU; pass-sharded over GPUs" % (20 * W * H, bounces),
+                "parallelism": "pass-shard x%d + RCCL gather" % world if world > 1 else "single GPU",
+                "nominal_mrays_per_s": round(nominal, 2),
+                "render_wall_ms_projected": round(ms_step * -(-P // world), 1),
+                "passes_per_frame": P,
+                "process_ms_per_step": round(proc_ms / max(args.steps, 1), 3),
+                "sort_ms_per_step": round(timed.get("sort_ms", 0.0) / max(args.steps, 1), 3),
+                "scene_load_s": round(load_s, 3),
+                "bvh_ms": round(scene.bvh_ms, 1),
+            },
+            "roofline": roof,
+            "cpu_baseline": None,
+        }
+        if counted:
+            out["config"]["counters"] = {k: counted[k] for k in ("live_segments", "nodes_popped", "internal_visits",
+                                                                 "triangle_tests", "hits", "misses", "dead_slots")}
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(cfg, args)
+            except Exception as e:  # reported, never fatal for the GPU numbers
+                out["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(out), flush=True)
+    ren.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -34,12 +34,35 @@ using namespace rtd;
 
 namespace {
 
+// Tuning knobs (compile-time; -D overrides are for A/B experiments only).
+#ifndef RT_STACK_LDS
+#define RT_STACK_LDS 8
+#endif
+#ifndef RT_REFILL
+#define RT_REFILL 16
+#endif
+#ifndef RT_CHUNK_MAX
+#define RT_CHUNK_MAX 128
+#endif
+#ifndef RT_TRI_BATCH
+#define RT_TRI_BATCH 4
+#endif
+#ifndef RT_QUEUES
+#define RT_QUEUES 8
+#endif
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
-constexpr int kStackLds = 16;         // stack entries per lane kept in LDS
+constexpr int kStackLds = RT_STACK_LDS; // stack entries per lane kept in LDS (deeper: global)
 constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138)
 constexpr int kSortItems = 16;        // sort tile = kBlock * kSortItems slots
 constexpr int kSortTile = kBlock * kSortItems;
 constexpr int kBuckets = 65;
+constexpr int kCtrSlots = 64;       // striped copies of the work counters
+constexpr int kChunkMax = RT_CHUNK_MAX; // slots a wave takes from the trace queue per atomic...
+constexpr int kChunkMin = 64;        // ...shrunk so that every wave gets ~4 chunks when few rays live
+constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are idle
+constexpr int kTriBatch = RT_TRI_BATCH; // leaf triangles whose loads are issued together
+constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
+constexpr int kQueueStride = 64;     // words between shards (256 B: one shard per cache line)
 constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFFFFF)
 constexpr uint32_t kLeaf = 0x80000000u, kBigLeaf = 0x40000000u;
 
@@ -58,7 +81,7 @@ struct DevScene {
 };
 
 struct Counters {                     // device-side work counters (u64, one atomic per wave)
-    unsigned long long live, pn, iv, tt, st, hits, misses, pad;
+    unsigned long long live, pn, iv, tt, st, hits, misses, hits_sphere;
 };
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
@@ -66,6 +89,10 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
     return s;
+}
+
+__device__ __forceinline__ uint32_t rank_below(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -92,22 +119,101 @@ __global__ __launch_bounds__(kBlock) void generate_kernel(DevScene S, float4 *__
 }
 
 // ---------------------------------------------------------------- traversal
-template <bool COUNT>
-struct Work { unsigned pn = 0, iv = 0, tt = 0; };
-
-// bvh_closest_hit_distance, scene.cu:134-241.  `col` = this lane's LDS stack column.
-template <bool COUNT>
-__device__ __forceinline__ void traverse(const DevScene &S, V3 o, V3 d, float &closest, int &index, uint2 *col,
-                                         Work<COUNT> &w) {
-    const float ix = 1 / d.x, iy = 1 / d.y, iz = 1 / d.z;
-    uint2 ovf[kStackMax - kStackLds];
-    uint32_t ref = S.root_ref;      // root is popped with distance 0 < closest
-    int sp = 0;
+// Closest hit for the live slots [0, *live): the sphere loop (scene.cu:338-372) and
+// bvh_closest_hit_distance (scene.cu:134-241).  Persistent and wave-refilling: each wave takes
+// chunks of slots from a device queue (one atomic per chunk) and hands a new slot to a lane
+// as soon as that lane's ray is done, so incoherent rays of very different traversal lengths
+// do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
+template <bool SORTED, bool COUNT>
+__global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, const float4 *__restrict__ rays,
+                                                       const uint32_t *__restrict__ idx,
+                                                       const uint8_t *__restrict__ bkt,
+                                                       const uint32_t *__restrict__ live_count,
+                                                       uint32_t *__restrict__ queue, float2 *__restrict__ hits,
+                                                       uint32_t *__restrict__ overflow, Counters *__restrict__ ctr) {
+    __shared__ uint2 stack[kStackLds * kBlock];
+    uint2 *col = stack + threadIdx.x;
+    // Overflow tail of the stack (entries >= kStackLds, rare) in a global per-lane buffer,
+    // [entry][lane] for coalescing; stored as two 32-bit arrays so the compiler cannot fuse the
+    // LDS and global pops into one flat load.
+    const size_t lanes = (size_t)gridDim.x * kBlock;
+    uint32_t *ovf_ref = overflow + (size_t)blockIdx.x * kBlock + threadIdx.x;
+    float *ovf_dist = reinterpret_cast<float *>(overflow + lanes * (kStackMax - kStackLds)) +
+                      (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t L = __builtin_amdgcn_readfirstlane(*live_count);
+    const uint32_t waves = gridDim.x * (kBlock / 64);
+    const uint32_t chunk = min((uint32_t)kChunkMax, max((uint32_t)kChunkMin, (L / (4 * waves) + 63) & ~63u));
+    // The live range is split into kQueues equal segments, each with its own queue word; a wave
+    // starts on the segment of its XCD group (blockIdx % 8) and moves on when that one is drained.
+    uint32_t shard = blockIdx.x % kQueues, tried = 0;
+    uint32_t q_next = 0, q_end = 0;     // this wave's current chunk (wave-uniform)
+    bool exhausted = false;
+    int slot = -1;                      // < 0: lane has no ray
+    V3 o{0, 0, 0}, d{0, 0, 0};
+    float ix = 0, iy = 0, iz = 0, closest = 0;
+    int index = -1, sp = 0;
+    uint32_t ref = 0;
+    unsigned pn = 0, iv = 0, tt = 0, nlive = 0;
     while (true) {
-        if (COUNT) w.pn++;
+        // ---- refill idle lanes (wave-uniform control flow)
+        unsigned long long idle = __ballot(slot < 0);
+        if (!exhausted && __popcll(idle) >= kRefill) {
+            bool fresh = false;
+            while (idle && !exhausted) {
+                if (q_next >= q_end) {
+                    const uint32_t seg_lo = (uint32_t)(((uint64_t)L * shard) / kQueues);
+                    const uint32_t seg_hi = (uint32_t)(((uint64_t)L * (shard + 1)) / kQueues);
+                    uint32_t c = 0;
+                    if (lane_id() == 0) c = atomicAdd(queue + shard * kQueueStride, chunk);
+                    c = __builtin_amdgcn_readfirstlane(__shfl(c, 0)) + seg_lo;
+                    if (c >= seg_hi) {
+                        shard = (shard + 1) % kQueues;
+                        if (++tried == kQueues) exhausted = true;
+                        continue;
+                    }
+                    q_next = c;
+                    q_end = min(c + chunk, seg_hi);
+                }
+                const uint32_t avail = q_end - q_next;
+                const uint32_t r = rank_below(idle);
+                const bool take = slot < 0 && r < avail;
+                const unsigned long long took = __ballot(take);
+                if (take) { slot = (int)(q_next + r); fresh = true; }
+                q_next += (uint32_t)__popcll(took);
+                idle &= ~took;
+            }
+            if (fresh) {
+                if (!SORTED && bkt[slot] == kDead) {
+                    slot = -1;          // no_sort: terminated rays stay in place
+                } else {
+                    nlive++;
+                    const float4 *rp = rays + (size_t)(SORTED ? idx[slot] : (uint32_t)slot) * 3;
+                    const float4 r0 = rp[0], r1 = rp[1];
+                    o = v3(r0.x, r0.y, r0.z);
+                    d = v3(r0.w, r1.x, r1.y);
+                    ix = 1 / d.x; iy = 1 / d.y; iz = 1 / d.z;
+                    closest = 1e30f;
+                    index = -1;
+                    for (int i = 0; i < S.sphere_count; i++) {
+                        const float4 sph = S.spheres[i];
+                        float t;
+                        if (ray_sphere(o, d, v3(sph.x, sph.y, sph.z), sph.w, closest, t)) { closest = t; index = i; }
+                    }
+                    ref = S.root_ref;   // root is popped with distance 0 < closest
+                    sp = 0;
+                }
+            }
+        }
+        if (!__ballot(slot >= 0)) {
+            if (exhausted) break;
+            continue;
+        }
+        if (slot < 0) continue;
+        // ---- one node visit
+        if (COUNT) pn++;
         bool descend = false;
         if (!(ref & kLeaf)) {
-            if (COUNT) w.iv++;
+            if (COUNT) iv++;
             const float4 *nd = S.nodes + (size_t)ref * 4;
             const float4 a = nd[0], b = nd[1], c = nd[2];
             const uint4 kids = *reinterpret_cast<const uint4 *>(nd + 3);
@@ -115,12 +221,17 @@ __device__ __forceinline__ void traverse(const DevScene &S, V3 o, V3 d, float &c
             const bool h0 = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, ix, iy, iz, closest, t0);
             const bool h1 = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, ix, iy, iz, closest, t1);
             if (h0 && h1) {
-                // Reference pushes near then far; the far child is popped next.
+                // The reference pushes near then far (scene.cu:204-225): the far child is next.
                 uint2 below;
                 float ttop;
                 if (t0 < t1) { below = make_uint2(kids.x, __float_as_uint(t0)); ref = kids.y; ttop = t1; }
                 else { below = make_uint2(kids.y, __float_as_uint(t1)); ref = kids.x; ttop = t0; }
-                if (sp < kStackLds) col[sp * kBlock] = below; else ovf[sp - kStackLds] = below;
+                if (__builtin_expect(sp < kStackLds, 1)) {
+                    col[sp * kBlock] = below;
+                } else {
+                    ovf_ref[(sp - kStackLds) * lanes] = below.x;
+                    ovf_dist[(sp - kStackLds) * lanes] = __uint_as_float(below.y);
+                }
                 sp++;
                 descend = !(ttop >= closest);
             } else if (h0) {
@@ -139,65 +250,98 @@ __device__ __forceinline__ void traverse(const DevScene &S, V3 o, V3 d, float &c
                 begin = (int)(ref & 0xFFFFFFu);
                 end = begin + (int)((ref >> 24) & 0x3Fu);
             }
-            for (int i = begin; i < end; i++) {       // Möller–Trumbore, scene.cu:160-195
-                if (COUNT) w.tt++;
-                const float4 *tp = S.tris + (size_t)i * 3;
-                const float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
-                const V3 p1 = v3(q0.x, q0.y, q0.z), e1 = v3(q0.w, q1.x, q1.y), e2 = v3(q1.z, q1.w, q2.x);
-                float t;
-                if (!ray_triangle(o, d, p1, e1, e2, closest, t)) continue;
-                closest = t;
-                index = S.sphere_count + i;
+            for (int i = begin; i < end; i += kTriBatch) {   // Möller–Trumbore, scene.cu:160-195
+                // Issue the loads of up to kTriBatch triangles before testing them in order.
+                float4 q[kTriBatch][3];
+#pragma unroll
+                for (int k = 0; k < kTriBatch; k++) {
+                    const float4 *tp = S.tris + (size_t)min(i + k, end - 1) * 3;
+                    q[k][0] = tp[0]; q[k][1] = tp[1]; q[k][2] = tp[2];
+                }
+#pragma unroll
+                for (int k = 0; k < kTriBatch; k++) {
+                    if (i + k < end) {
+                        if (COUNT) tt++;
+                        float t;
+                        if (ray_triangle(o, d, v3(q[k][0].x, q[k][0].y, q[k][0].z), v3(q[k][0].w, q[k][1].x, q[k][1].y),
+                                         v3(q[k][1].z, q[k][1].w, q[k][2].x), closest, t)) {
+                            closest = t;
+                            index = S.sphere_count + i + k;
+                        }
+                    }
+                }
             }
         }
-        if (descend) continue;
-        bool found = false;
-        while (sp > 0) {
-            sp--;
-            const uint2 e = sp < kStackLds ? col[sp * kBlock] : ovf[sp - kStackLds];
-            if (!(__uint_as_float(e.y) >= closest)) { ref = e.x; found = true; break; }
+        if (!descend) {
+            bool found = false;
+            while (sp > 0) {
+                sp--;
+                uint32_t eref;
+                float edist;
+                if (__builtin_expect(sp < kStackLds, 1)) {
+                    const uint2 e = col[sp * kBlock];
+                    eref = e.x;
+                    edist = __uint_as_float(e.y);
+                } else {
+                    eref = ovf_ref[(sp - kStackLds) * lanes];
+                    edist = ovf_dist[(sp - kStackLds) * lanes];
+                }
+                if (!(edist >= closest)) { ref = eref; found = true; break; }
+            }
+            if (!found) {
+                hits[slot] = make_float2(closest, __int_as_float(index));
+                slot = -1;
+            }
         }
-        if (!found) break;
     }
+    Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
+    const unsigned long long nl = wave_sum(nlive);
+    if (COUNT) {
+        const unsigned long long a = wave_sum(pn), b = wave_sum(iv), t = wave_sum(tt);
+        if (lane_id() == 0) {
+            atomicAdd(&cs->pn, a);
+            atomicAdd(&cs->iv, b);
+            atomicAdd(&cs->tt, t);
+            atomicAdd(&cs->st, nl * (unsigned long long)S.sphere_count);
+        }
+    }
+    if (lane_id() == 0 && nl) atomicAdd(&cs->live, nl);
 }
 
-// One bounce for one slot: raytracing.cu:83-94 -> Scene::process_ray (scene.cu:320-487).
+// Shading for the live slots (scene.cu:376-485): environment lookup on a miss, otherwise
+// emission + scatter; then the new ray state and its reorder bucket.  One lane per slot.
 template <bool SORTED, bool COUNT>
-__global__ __launch_bounds__(kBlock) void process_kernel(DevScene S, float4 *__restrict__ rays,
-                                                         const uint32_t *__restrict__ idx, uint8_t *__restrict__ bkt,
-                                                         int n, uint32_t seed_term, Counters *__restrict__ ctr) {
-    __shared__ uint2 stack[kStackLds * kBlock];
-    const int slot = blockIdx.x * kBlock + threadIdx.x;
-    const bool live = slot < n && bkt[slot] != kDead;
-    Work<COUNT> w;
-    unsigned hit = 0, miss = 0;
-    if (live) {
-        Rng rng = pcg_seed((uint32_t)slot * 4137874753u + seed_term);
-        const uint32_t ri = SORTED ? idx[slot] : (uint32_t)slot;
-        float4 *rp = rays + (size_t)ri * 3;
+__global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, float4 *__restrict__ rays,
+                                                       const uint32_t *__restrict__ idx, uint8_t *__restrict__ bkt,
+                                                       const uint32_t *__restrict__ live_count,
+                                                       const float2 *__restrict__ hits, uint32_t seed_term,
+                                                       Counters *__restrict__ ctr) {
+    const int L = (int)__builtin_amdgcn_readfirstlane(*live_count);
+    unsigned hit = 0, miss = 0, hit_sphere = 0;
+    for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
+        const int slot = base + threadIdx.x;
+        if (slot >= L || bkt[slot] == kDead) continue;
+        Rng rng = pcg_seed((uint32_t)slot * 4137874753u + seed_term);   // raytracing.cu:89
+        const float2 h = hits[slot];
+        const float closest = h.x;
+        const int index = __float_as_int(h.y);
+        float4 *rp = rays + (size_t)(SORTED ? idx[slot] : (uint32_t)slot) * 3;
         const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
         const V3 o = v3(r0.x, r0.y, r0.z), d = v3(r0.w, r1.x, r1.y);
         V3 T = v3(r1.z, r1.w, r2.x), C = v3(r2.y, r2.z, r2.w);
-        float closest = 1e30f;
-        int index = -1;
-        for (int i = 0; i < S.sphere_count; i++) {   // scene.cu:338-372
-            const float4 sp = S.spheres[i];
-            float t;
-            if (ray_sphere(o, d, v3(sp.x, sp.y, sp.z), sp.w, closest, t)) { closest = t; index = i; }
-        }
-        traverse<COUNT>(S, o, d, closest, index, stack + threadIdx.x, w);
         V3 no = o, nd = d;
-        if (index == -1) {                             // scene.cu:376-395
-            miss = 1;
+        if (index == -1) {
+            miss++;
             C = C + sky_color(S.env, S.env_w, S.env_h, d) * T;
             T = v3(0, 0, 0);
         } else {
-            hit = 1;
+            hit++;
             no = o + closest * d;
             V3 normal;
             if (index < S.sphere_count) {
-                const float4 sp = S.spheres[index];
-                normal = (1 / sp.w) * (no - v3(sp.x, sp.y, sp.z));
+                hit_sphere++;
+                const float4 sph = S.spheres[index];
+                normal = (1 / sph.w) * (no - v3(sph.x, sph.y, sph.z));
             } else {
                 const float4 q2 = S.tris[(size_t)(index - S.sphere_count) * 3 + 2];
                 normal = v3(q2.y, q2.z, q2.w);
@@ -209,21 +353,23 @@ __global__ __launch_bounds__(kBlock) void process_kernel(DevScene S, float4 *__r
         rp[2] = make_float4(T.z, C.x, C.y, C.z);
         bkt[slot] = (uint8_t)(is_black(T) ? kDead : bucket_of(no, nd, S.min_coord, S.inv_dim));
     }
-    const unsigned long long nlive = __popcll(__ballot(live));
-    if (lane_id() == 0 && nlive) atomicAdd(&ctr->live, nlive);
     if (COUNT) {
-        const unsigned long long a = wave_sum(w.pn), b = wave_sum(w.iv), c = wave_sum(w.tt);
-        const unsigned long long h = wave_sum(hit), m = wave_sum(miss);
-        if (lane_id() == 0 && nlive) {
-            atomicAdd(&ctr->pn, a);
-            atomicAdd(&ctr->iv, b);
-            atomicAdd(&ctr->tt, c);
-            atomicAdd(&ctr->hits, h);
-            atomicAdd(&ctr->misses, m);
-            atomicAdd(&ctr->st, nlive * (unsigned long long)S.sphere_count);
+        Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
+        const unsigned long long h = wave_sum(hit), m = wave_sum(miss), hs = wave_sum(hit_sphere);
+        if (lane_id() == 0 && (h | m)) {
+            atomicAdd(&cs->hits, h);
+            atomicAdd(&cs->misses, m);
+            atomicAdd(&cs->hits_sphere, hs);
         }
     }
 }
+
+__global__ void fill_live_kernel(uint32_t *__restrict__ live, uint32_t n, int count, uint32_t *__restrict__ queue) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) live[i] = n;
+    for (int k = i; k < count * kQueues * kQueueStride; k += blockDim.x) queue[k] = 0;
+}
+
 
 // ---------------------------------------------------------------- stable 65-bucket reorder
 // Equivalent to cub::DeviceRadixSort::SortPairs on the reference keys (raytracing.cu:238-247).
@@ -238,13 +384,12 @@ __device__ __forceinline__ unsigned long long match_bucket(uint32_t b, bool vali
     return peers;
 }
 
-__device__ __forceinline__ uint32_t rank_below(unsigned long long mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
 // Per-tile bucket counts, written bucket-major: counts[b * tiles + tile].
-__global__ __launch_bounds__(kBlock) void sort_hist_kernel(const uint8_t *__restrict__ bkt, int n, int tiles,
+__global__ __launch_bounds__(kBlock) void sort_hist_kernel(const uint8_t *__restrict__ bkt,
+                                                           const uint32_t *__restrict__ live_count, int tiles,
                                                            uint32_t *__restrict__ counts) {
+    const int n = (int)*live_count;
+    if ((int)blockIdx.x * kSortTile >= n) return;
     __shared__ uint32_t h[kBuckets];
     for (int b = threadIdx.x; b < kBuckets; b += kBlock) h[b] = 0;
     __syncthreads();
@@ -262,13 +407,18 @@ __global__ __launch_bounds__(kBlock) void sort_hist_kernel(const uint8_t *__rest
 }
 
 // One workgroup per bucket: exclusive scan of that bucket's tile counts + bucket total.
-__global__ __launch_bounds__(kBlock) void sort_scan_kernel(const uint32_t *__restrict__ counts, int tiles,
-                                                           uint32_t *__restrict__ offsets, uint32_t *__restrict__ totals) {
+__global__ __launch_bounds__(kBlock) void sort_scan_kernel(const uint32_t *__restrict__ counts,
+                                                           const uint32_t *__restrict__ live_count, int tiles_max,
+                                                           uint32_t *__restrict__ offsets, uint32_t *__restrict__ totals,
+                                                           uint32_t *__restrict__ live_next) {
+    const uint32_t n = *live_count;
+    const int tiles = (int)((n + kSortTile - 1) / kSortTile);
+    (void)tiles_max;
     __shared__ uint32_t wsum[kBlock / 64];
     __shared__ uint32_t carry;
     const int b = blockIdx.x;
-    const uint32_t *in = counts + (size_t)b * tiles;
-    uint32_t *out = offsets + (size_t)b * tiles;
+    const uint32_t *in = counts + (size_t)b * tiles_max;
+    uint32_t *out = offsets + (size_t)b * tiles_max;
     if (threadIdx.x == 0) carry = 0;
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -290,16 +440,22 @@ __global__ __launch_bounds__(kBlock) void sort_scan_kernel(const uint32_t *__res
         if (threadIdx.x == kBlock - 1) carry = pre + x;
         __syncthreads();
     }
-    if (threadIdx.x == 0) totals[b] = carry;
+    if (threadIdx.x == 0) {
+        totals[b] = carry;
+        if (b == (int)kDead) *live_next = n - carry;   // rays still live after this bounce
+    }
 }
 
 // Stable scatter: rounds of 256 consecutive slots; rank = earlier rounds + earlier waves +
 // earlier lanes holding the same bucket.
 __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__restrict__ bkt_in,
-                                                              const uint32_t *__restrict__ idx_in, int n, int tiles,
+                                                              const uint32_t *__restrict__ idx_in,
+                                                              const uint32_t *__restrict__ live_count, int tiles,
                                                               const uint32_t *__restrict__ offsets,
                                                               const uint32_t *__restrict__ totals,
                                                               uint8_t *__restrict__ bkt_out, uint32_t *__restrict__ idx_out) {
+    const int n = (int)*live_count;
+    if ((int)blockIdx.x * kSortTile >= n) return;
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
     if (threadIdx.x == 0) {
@@ -452,10 +608,14 @@ struct rt_renderer {
     DevBuf<uint16_t> mat_idx;
     DevBuf<int2> big;
     DevBuf<float> env, fb;
-    DevBuf<uint32_t> idx[2], sort_counts, sort_offsets, sort_totals;
+    DevBuf<uint32_t> idx[2], sort_counts, sort_offsets, sort_totals, live, queue;
+    DevBuf<float2> hits;
+    DevBuf<uint32_t> overflow;        // traversal stack overflow, 2 x (kStackMax - kStackLds) words per lane
     DevBuf<uint8_t> bkt[2];
     DevBuf<Counters> ctr;
     std::vector<hipEvent_t> events;
+    int resident_blocks = 0;          // trace_kernel workgroups resident on the whole chip
+    int cus = 0;
     hipEvent_t t_begin = nullptr, t_end = nullptr;
 
     ~rt_renderer() {
@@ -537,7 +697,15 @@ struct rt_renderer {
             if ((rc = sort_offsets.alloc((size_t)kBuckets * tiles))) return rc;
             if ((rc = sort_totals.alloc(kBuckets))) return rc;
         }
-        if ((rc = ctr.alloc(1))) return rc;
+        if ((rc = ctr.alloc(kCtrSlots))) return rc;
+        if ((rc = live.alloc((size_t)bounces + 1))) return rc;
+        if ((rc = queue.alloc((size_t)(bounces + 1) * kQueues * kQueueStride))) return rc;
+        if ((rc = hits.alloc((size_t)max_rays))) return rc;
+        int per_cu = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<true, false>, kBlock, 0));
+        resident_blocks = std::max(1, cus * std::max(1, per_cu));
+        if ((rc = overflow.alloc((size_t)resident_blocks * kBlock * 2 * (kStackMax - kStackLds)))) return rc;
         HIPCHK(hipMemsetAsync(fb.p, 0, fb.n * sizeof(float), stream));
         ds.spheres = spheres.p;
         ds.tris = tris.p;
@@ -582,6 +750,9 @@ struct rt_renderer {
         const int grid = blocks_for(n);
         const int tiles = (n + kSortTile - 1) / kSortTile;
         int cur = 0;
+        const int tgrid = std::min(grid, resident_blocks);
+        const int sgrid = std::min(grid, cus * 8);
+        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, stream, live.p, (uint32_t)n, bounces + 1, queue.p);
         hipLaunchKernelGGL(generate_kernel, dim3(grid), dim3(kBlock), 0, stream, ds, rays.p, idx[0].p, bkt[0].p, rtc, n,
                            709579u * (uint32_t)remaining);
         for (int b = 0; b < bounces; b++) {
@@ -589,32 +760,31 @@ struct rt_renderer {
             hipEvent_t e0 = event(ev++), e1 = event(ev++);
             if (!e0 || !e1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
             HIPCHK(hipEventRecord(e0, stream));
+            const uint32_t *lv = live.p + b;
+#define RT_PROCESS(SORTED, COUNT)                                                                               \
+    do {                                                                                                        \
+        hipLaunchKernelGGL((trace_kernel<SORTED, COUNT>), dim3(tgrid), dim3(kBlock), 0, stream, ds, rays.p,      \
+                           idx[cur].p, bkt[cur].p, lv, queue.p + (size_t)b * kQueues * kQueueStride, hits.p, overflow.p, ctr.p);                 \
+        hipLaunchKernelGGL((shade_kernel<SORTED, COUNT>), dim3(sgrid), dim3(kBlock), 0, stream, ds, rays.p,      \
+                           idx[cur].p, bkt[cur].p, lv, hits.p, seed_term, ctr.p);                               \
+    } while (0)
             if (sort) {
-                if (counters)
-                    hipLaunchKernelGGL((process_kernel<true, true>), dim3(grid), dim3(kBlock), 0, stream, ds, rays.p,
-                                       idx[cur].p, bkt[cur].p, n, seed_term, ctr.p);
-                else
-                    hipLaunchKernelGGL((process_kernel<true, false>), dim3(grid), dim3(kBlock), 0, stream, ds, rays.p,
-                                       idx[cur].p, bkt[cur].p, n, seed_term, ctr.p);
+                if (counters) RT_PROCESS(true, true); else RT_PROCESS(true, false);
             } else {
-                if (counters)
-                    hipLaunchKernelGGL((process_kernel<false, true>), dim3(grid), dim3(kBlock), 0, stream, ds, rays.p,
-                                       idx[cur].p, bkt[cur].p, n, seed_term, ctr.p);
-                else
-                    hipLaunchKernelGGL((process_kernel<false, false>), dim3(grid), dim3(kBlock), 0, stream, ds, rays.p,
-                                       idx[cur].p, bkt[cur].p, n, seed_term, ctr.p);
+                if (counters) RT_PROCESS(false, true); else RT_PROCESS(false, false);
             }
+#undef RT_PROCESS
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(e1, stream));
             if (sort && b + 1 != bounces) {
                 hipEvent_t s0 = event(ev++), s1 = event(ev++);
                 if (!s0 || !s1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
                 HIPCHK(hipEventRecord(s0, stream));
-                hipLaunchKernelGGL(sort_hist_kernel, dim3(tiles), dim3(kBlock), 0, stream, bkt[cur].p, n, tiles,
+                hipLaunchKernelGGL(sort_hist_kernel, dim3(tiles), dim3(kBlock), 0, stream, bkt[cur].p, lv, tiles,
                                    sort_counts.p);
-                hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, stream, sort_counts.p, tiles,
-                                   sort_offsets.p, sort_totals.p);
-                hipLaunchKernelGGL(sort_scatter_kernel, dim3(tiles), dim3(kBlock), 0, stream, bkt[cur].p, idx[cur].p, n,
+                hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, stream, sort_counts.p, lv, tiles,
+                                   sort_offsets.p, sort_totals.p, live.p + b + 1);
+                hipLaunchKernelGGL(sort_scatter_kernel, dim3(tiles), dim3(kBlock), 0, stream, bkt[cur].p, idx[cur].p, lv,
                                    tiles, sort_offsets.p, sort_totals.p, bkt[1 - cur].p, idx[1 - cur].p);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventRecord(s1, stream));
@@ -636,7 +806,7 @@ struct rt_renderer {
         if (count < 0) count = pass_begin < P ? (P - pass_begin + stride - 1) / stride : 0;
         if (pass_begin < 0 || (count > 0 && pass_begin + (int64_t)(count - 1) * stride >= P))
             return rtamd::fail(RT_E_INVALID, "pass range outside the render");
-        HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters), stream));
+        HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, stream));
         HIPCHK(hipEventRecord(t_begin, stream));
         size_t ev = 0;
         int64_t sorted = 0, generated = 0;
@@ -651,8 +821,13 @@ struct rt_renderer {
         HIPCHK(hipStreamSynchronize(stream));
         if (st) {
             std::memset(st, 0, sizeof(*st));
-            Counters c;
-            HIPCHK(hipMemcpy(&c, ctr.p, sizeof(c), hipMemcpyDeviceToHost));
+            std::vector<Counters> slots(kCtrSlots);
+            HIPCHK(hipMemcpy(slots.data(), ctr.p, sizeof(Counters) * kCtrSlots, hipMemcpyDeviceToHost));
+            Counters c{};
+            for (const Counters &x : slots) {
+                c.live += x.live; c.pn += x.pn; c.iv += x.iv; c.tt += x.tt; c.st += x.st;
+                c.hits += x.hits; c.misses += x.misses; c.hits_sphere += x.hits_sphere;
+            }
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, t_begin, t_end));
             st->kernel_ms = ms;
@@ -681,6 +856,8 @@ struct rt_renderer {
             st->sphere_tests = c.st;
             st->hits = c.hits;
             st->misses = c.misses;
+            st->hits_sphere = c.hits_sphere;
+            st->dead_slots = (uint64_t)generated * bounces - c.live;
             st->passes = (uint32_t)count;
             st->render_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
         }

@@ -13,7 +13,7 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 BUILD_DIR = os.path.join(PKG_DIR, "build")
-LIB_PATH = os.path.join(BUILD_DIR, "librtamd.so")
+LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(BUILD_DIR, "librtamd.so")  # env: A/B builds only
 CLI_PATH = os.path.join(BUILD_DIR, "raytracing")
 HEADER = os.path.join(REPO, "include", "rt_abi.h")
 ASSETS = os.path.join(REPO, "assets")
@@ -58,7 +58,8 @@ class RtOpts(C.Structure):
 class RtStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("generated_rays", "live_segments", "sorted_items",
                                           "nodes_popped", "internal_visits", "triangle_tests",
-                                          "sphere_tests", "hits", "misses")] + \
+                                          "sphere_tests", "hits", "misses", "hits_sphere",
+                                          "dead_slots")] + \
                [("passes", C.c_uint32), ("reserved", C.c_uint32)] + \
                [(n, C.c_double) for n in ("render_ms", "kernel_ms", "process_ms", "sort_ms")]
 

@@ -108,7 +108,9 @@ typedef struct {
     uint64_t internal_visits;  /* Iv, only with collect_counters                           */
     uint64_t triangle_tests;   /* Tt, only with collect_counters                           */
     uint64_t sphere_tests;     /* S x live segments                                        */
-    uint64_t hits, misses;
+    uint64_t hits, misses;     /* closest-hit outcomes over live segments                  */
+    uint64_t hits_sphere;      /* subset of hits on spheres (the rest hit triangles)       */
+    uint64_t dead_slots;       /* slots skipped by the terminated-key early-out            */
     uint32_t passes, reserved;
     double render_ms;          /* host wall time of the call (the "GPU Took" span)         */
     double kernel_ms;          /* HIP-event time of the whole pass loop on the stream      */

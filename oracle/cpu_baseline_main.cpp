@@ -28,14 +28,16 @@ int main(int argc, char **argv) {
     orc_get_info(s, &info);
     std::vector<float> fb((size_t)info.width * info.height * 3);
     double secs = 0;
-    const int passes = orc_render_cpu_path(s, fb.data(), pass_limit, threads, &secs);
+    uint64_t live = 0;
+    const int passes = orc_render_cpu_path_counted(s, fb.data(), pass_limit, threads, &secs, &live);
     double mean = 0;
     for (float v : fb) mean += v;
     mean /= fb.size();
     std::printf("CPU Took %gs\n", secs);
     std::printf("{\"seconds\": %.6f, \"passes\": %d, \"threads\": %d, \"width\": %d, \"height\": %d, "
-                "\"spp\": %d, \"bounces\": %d, \"fb_mean\": %.6g}\n",
-                secs, passes, threads, info.width, info.height, info.ray_count, info.bounces, mean);
+                "\"spp\": %d, \"bounces\": %d, \"live_segments\": %llu, \"fb_mean\": %.6g}\n",
+                secs, passes, threads, info.width, info.height, info.ray_count, info.bounces,
+                (unsigned long long)live, mean);
     orc_free_scene(s);
     return 0;
 }

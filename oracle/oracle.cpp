@@ -509,10 +509,11 @@ inline bool ray_sphere(const Sphere &sp, V3 o, V3 d, float closest, float *t_out
 
 struct Counters {
     uint64_t pn = 0, iv = 0, tt = 0, st = 0, ht = 0, hs = 0, miss = 0, live = 0, dead = 0;
-    uint32_t max_stack = 0;
+    uint32_t max_stack = 0, max_ray_pn = 0;
     void add(const Counters &o) {
         pn += o.pn; iv += o.iv; tt += o.tt; st += o.st; ht += o.ht; hs += o.hs; miss += o.miss;
         live += o.live; dead += o.dead; max_stack = std::max(max_stack, o.max_stack);
+        max_ray_pn = std::max(max_ray_pn, o.max_ray_pn);
     }
 };
 
@@ -614,7 +615,9 @@ void process_ray(const orc_scene *s, RayData *rp, uint32_t *key, Rng rng, bool g
         float t;
         if (ray_sphere(s->spheres[i], o, d, closest, &t)) { closest = t; index = i; }
     }
+    const uint64_t pn0 = c.pn;
     bvh_closest_hit(s, o, d, closest, index, c);
+    c.max_ray_pn = std::max(c.max_ray_pn, (uint32_t)(c.pn - pn0));
     if (index == -1) {
         c.miss++;
         const V3 sky = s->env[env_texel(s, d)];
@@ -854,6 +857,7 @@ int orc_render_gpu_semantics(const orc_scene *s, int sort, int pass_begin, int p
         stats->misses = total.miss;
         stats->sorted_items = sorted;
         stats->max_stack = total.max_stack;
+        stats->max_ray_nodes = total.max_ray_pn;
         stats->passes = (uint32_t)pass_count;
     }
     return 0;
@@ -874,6 +878,11 @@ int orc_render_pass_sums(const orc_scene *s, int sort, int pass_begin, int pass_
 // raytracing.cu:122-163 (timed span = "CPU Took").  The inner loop's `i` shadows the bounce index,
 // so the seed does not depend on the bounce (raytracing.cu:142-149).
 int orc_render_cpu_path(const orc_scene *s, float *fb, int pass_limit, int threads, double *seconds) {
+    return orc_render_cpu_path_counted(s, fb, pass_limit, threads, seconds, nullptr);
+}
+
+int orc_render_cpu_path_counted(const orc_scene *s, float *fb, int pass_limit, int threads, double *seconds,
+                                uint64_t *live_out) {
     const auto t0 = std::chrono::high_resolution_clock::now();
     const int nt = nthreads(threads);
     const int64_t pixels = (int64_t)s->width * s->height;
@@ -889,13 +898,16 @@ int orc_render_cpu_path(const orc_scene *s, float *fb, int pass_limit, int threa
 #pragma omp parallel for schedule(dynamic, 1000) num_threads(nt)
         for (int i = 0; i < total; i++) generate_ray(s, rays.data(), nullptr, nullptr, rtc, i, remaining);
         for (int b = 0; b < s->bounces; b++) {
-#pragma omp parallel for schedule(dynamic, 1000) num_threads(nt)
+            uint64_t live = 0;
+#pragma omp parallel for schedule(dynamic, 1000) num_threads(nt) reduction(+ : live)
             for (int i = 0; i < total; i++) {
                 Rng rng;
                 xor_srand(&rng, 1905678123u * (uint32_t)i + 345903u * (uint32_t)(remaining * 20 + i));
                 Counters c;
                 process_ray(s, &rays[i], nullptr, rng, false, c);
+                live += c.live;
             }
+            if (live_out) *live_out += live;
         }
         for (int i = 0; i < total; i++) {                    // raytracing.cu:114-120
             float *p = fb + (size_t)(i / rtc) * 3;

@@ -45,6 +45,8 @@ typedef struct {
     uint64_t sorted_items;
     uint32_t max_stack;
     uint32_t passes;
+    uint32_t max_ray_nodes;     /* largest Pn of a single segment                */
+    uint32_t reserved;
 } orc_stats;
 
 /* Scene loading (restates scene.cu:491-831 + generate_bvh 1002-1036).
@@ -81,6 +83,9 @@ int orc_render_pass_sums(const orc_scene *s, int sort, int pass_begin, int pass_
  * no sort, sequential accumulate.  fb_out: W*H*3 (overwritten). pass_limit < 0 = all. */
 int orc_render_cpu_path(const orc_scene *s, float *fb_out, int pass_limit, int threads,
                         double *seconds);
+/* Same, also counting live ray segments (process_ray calls past the early-out). */
+int orc_render_cpu_path_counted(const orc_scene *s, float *fb_out, int pass_limit, int threads,
+                                double *seconds, uint64_t *live_segments);
 
 /* Post-process (raytracing.cu:21-74, 286-303). */
 void orc_bloom(float *fb, int width, int height, float threshold, int radius);

@@ -22,7 +22,8 @@ class OrcStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "generated_rays", "live_segments", "dead_slots", "nodes_popped", "internal_visits",
         "triangle_tests", "sphere_tests", "hits_triangle", "hits_sphere", "misses",
-        "sorted_items")] + [("max_stack", C.c_uint32), ("passes", C.c_uint32)]
+        "sorted_items")] + [("max_stack", C.c_uint32), ("passes", C.c_uint32),
+                                     ("max_ray_nodes", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
