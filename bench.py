@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--cpu-spp", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-counters", action="store_true", help="skip the byte-model counting rerun")
+    ap.add_argument("--dist", action="store_true", help="use the torch.distributed path even at N=1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,7 +111,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     torch = None
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -129,15 +135,23 @@ def main():
     ren = rtamd.Renderer(scene, sort=sort, device=local)
 
     px3 = W * H * 3
-    pass_buf = gather = fb_acc = None
-    if world > 1:
-        pass_buf = torch.empty(px3, dtype=torch.float32, device="cuda")
-        if rank == 0:
-            gather = [torch.empty(px3, dtype=torch.float32, device="cuda") for _ in range(world)]
-            fb_acc = torch.zeros(px3, dtype=torch.float32, device="cuda")
+    frame = None
+    stats_acc = {}
+
+    def render_pass(p, out):
+        st = ren.run(pass_begin=p, count=1, d_pass_sums=out.data_ptr() if out is not None else None)
+        for k in ("live_segments", "generated_rays"):
+            stats_acc[k] = stats_acc.get(k, 0) + st[k]
+        for k in ("process_ms", "sort_ms", "kernel_ms"):
+            stats_acc[k] = stats_acc.get(k, 0.0) + st[k]
+
+    if use_dist:
+        import rtamd_dist
+        frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, torch.device("cuda", local), render_pass)
+        n_rounds = rtamd_dist.rounds(world, P)
 
     def barrier_sync():
-        if world > 1:
+        if use_dist:
             dist.barrier()
             torch.cuda.synchronize()
 
@@ -145,19 +159,15 @@ def main():
         return (rank + world * step) % P
 
     def one_step(step, stats):
-        st = ren.run(pass_begin=pass_of(step), count=1,
-                     d_pass_sums=pass_buf.data_ptr() if pass_buf is not None else None)
-        for k in ("live_segments", "generated_rays"):
-            stats[k] = stats.get(k, 0) + st[k]
-        stats["process_ms"] = stats.get("process_ms", 0.0) + st["process_ms"]
-        stats["sort_ms"] = stats.get("sort_ms", 0.0) + st["sort_ms"]
-        stats["kernel_ms"] = stats.get("kernel_ms", 0.0) + st["kernel_ms"]
-        if world > 1:
-            # RCCL gather of every rank's pass framebuffer; rank 0 adds them in pass order.
-            dist.gather(pass_buf, gather_list=gather, dst=0)
-            if rank == 0:
-                for g in gather:
-                    fb_acc.add_(g)
+        stats_acc.clear()
+        if use_dist:
+            # render this rank's pass of round `step`, RCCL-gather the round's pass framebuffers
+            # to rank 0, which adds them in pass order (rtamd_dist.PassShardedFrame)
+            frame.run_round(step % n_rounds)
+        else:
+            render_pass(pass_of(step), None)
+        for k, v in stats_acc.items():
+            stats[k] = stats.get(k, 0) + v
 
     warm = {}
     for s in range(args.warmup):
@@ -172,7 +182,7 @@ def main():
 
     live = timed.get("live_segments", 0)
     proc_ms = timed.get("process_ms", 0.0)
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -251,7 +261,7 @@ def main():
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)
     ren.close()
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -1,0 +1,60 @@
+"""The C ABI boundary (include/rt_abi.h): library loads, exports every declared symbol, and the
+ctypes mirror matches the C struct layouts.  No HIP compute calls (runs without a GPU)."""
+import ctypes as C
+import re
+import subprocess
+
+import rtamd as R
+
+
+def declared_functions():
+    text = open(R.HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_drop_in_entry_points():
+    names = declared_functions()
+    for n in ("rt_render", "rt_scene_load", "rt_bloom", "rt_tonemap", "rt_write_png", "rt_cpu_render",
+              "rt_renderer_create", "rt_renderer_run", "rt_last_error"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = R.lib()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", R.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(line.split()[-1] for line in out.splitlines())
+    assert set(declared_functions()) <= exported
+
+
+def test_library_is_gfx950_and_links_hip():
+    blob = open(R.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}
+    ldd = subprocess.run(["ldd", R.LIB_PATH], capture_output=True, text=True).stdout
+    assert "libamdhip64" in ldd
+
+
+def test_struct_layouts():
+    # sizes fixed by the reference layouts (scene.cuh:9-100) and by rt_abi.h
+    assert C.sizeof(R.RtScene) == 216
+    assert C.sizeof(R.RtOpts) == 24
+    assert C.sizeof(R.RtLoadOpts) == 48
+    assert C.sizeof(R.RtStats) == 11 * 8 + 8 + 4 * 8
+    assert R.lib().rt_abi_version() == 1
+
+
+def test_default_options():
+    o = R.RtOpts()
+    R.lib().rt_default_opts(C.byref(o))
+    assert (o.sort, o.device, o.pass_begin, o.pass_count, o.pass_stride, o.collect_counters) == (1, 0, 0, -1, 1, 0)
+
+
+def test_invalid_arguments_fail_loudly():
+    lib = R.lib()
+    assert lib.rt_render(None, None, None, None) < 0
+    assert b"null" in lib.rt_last_error()
+    assert lib.rt_renderer_run(None, 0, 1, 1, None, None) < 0
+    assert lib.rt_write_png(b"/nonexistent/x.png", None, 1, 1) < 0

@@ -1,0 +1,57 @@
+"""N>1 path on CPU: world_size-2 gloo process group running the same pass-sharding and ordered
+gather code (rtamd_dist.PassShardedFrame) that bench.py runs over RCCL.  Pass sums come from the
+oracle here (the GPU renders them on the box); the assembled frame must be bit-identical to
+the single-process render."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle_lib as O
+import rtamd_dist as D
+
+IMAGE = (24, 16, 100, 4)       # 5 passes: uneven over 2 ranks
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = O.OracleScene(os.path.join(O.ASSETS, "cornell_plus.scene"), image=IMAGE)
+
+    def render_pass(p, out):
+        out.copy_(torch.from_numpy(sc.pass_sums(sort=True, pass_begin=p, pass_count=1, threads=2)[0]))
+
+    frame = D.PassShardedFrame(dist, torch, sc.pixels * 3, sc.passes, "cpu", render_pass)
+    n = frame.run_all()
+    assert n == len(D.pass_schedule(rank, world, sc.passes))
+    if rank == 0:
+        np.save(out_path, frame.fb.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pass_sharded_frame_is_bitexact(tmp_path, world):
+    out = str(tmp_path / "fb.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    ref, _ = O.OracleScene(os.path.join(O.ASSETS, "cornell_plus.scene"), image=IMAGE).render(sort=True)
+    assert np.array_equal(got, ref)
+
+
+def test_schedule_covers_every_pass_once():
+    for world in (1, 2, 3, 8):
+        for passes in (1, 5, 103, 205):
+            got = sorted(p for r in range(world) for p in D.pass_schedule(r, world, passes))
+            assert got == list(range(passes))
