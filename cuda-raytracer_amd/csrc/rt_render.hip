@@ -47,6 +47,12 @@ namespace {
 #ifndef RT_TRI_BATCH
 #define RT_TRI_BATCH 4
 #endif
+#ifndef RT_INFLIGHT
+#define RT_INFLIGHT 4
+#endif
+#ifndef RT_TRACE_OCC
+#define RT_TRACE_OCC 75
+#endif
 #ifndef RT_QUEUES
 #define RT_QUEUES 8
 #endif
@@ -61,6 +67,8 @@ constexpr int kChunkMax = RT_CHUNK_MAX; // slots a wave takes from the trace que
 constexpr int kChunkMin = 64;        // ...shrunk so that every wave gets ~4 chunks when few rays live
 constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are idle
 constexpr int kTriBatch = RT_TRI_BATCH; // leaf triangles whose loads are issued together
+constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffer set each)
+constexpr int kTraceOccPct = RT_TRACE_OCC; // % of the resident trace workgroups the persistent grid uses
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
 constexpr int kQueueStride = 64;     // words between shards (256 B: one shard per cache line)
 constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFFFFF)
@@ -495,10 +503,10 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
 }
 
 // ---------------------------------------------------------------- accumulate
-// Ordered per-pixel sum of the pass's samples, then fb += sum (raytracing.cu:96-107 without
+// Ordered per-pixel sum of the pass's samples (the caller then adds it: fb += sum, in pass order) (raytracing.cu:96-107 without
 // the unordered atomics; the CPU path's order, raytracing.cu:114-120).
-__global__ __launch_bounds__(kBlock) void accumulate_kernel(float *__restrict__ fb, const float4 *__restrict__ rays,
-                                                            int rtc, int pixels, float *__restrict__ pass_out) {
+__global__ __launch_bounds__(kBlock) void accumulate_kernel(const float4 *__restrict__ rays, int rtc, int pixels,
+                                                            float *__restrict__ sums) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= pixels) return;
     float sx = 0, sy = 0, sz = 0;
@@ -509,15 +517,9 @@ __global__ __launch_bounds__(kBlock) void accumulate_kernel(float *__restrict__ 
         sy = sy + c.z;
         sz = sz + c.w;
     }
-    float *f = fb + (size_t)p * 3;
-    f[0] = f[0] + sx;
-    f[1] = f[1] + sy;
-    f[2] = f[2] + sz;
-    if (pass_out) {
-        pass_out[(size_t)p * 3] = sx;
-        pass_out[(size_t)p * 3 + 1] = sy;
-        pass_out[(size_t)p * 3 + 2] = sz;
-    }
+    sums[(size_t)p * 3] = sx;
+    sums[(size_t)p * 3 + 1] = sy;
+    sums[(size_t)p * 3 + 2] = sz;
 }
 
 // ---------------------------------------------------------------- bloom (raytracing.cu:21-74)
@@ -598,33 +600,56 @@ bool is_leaf(const rt_bvh_node &nd) { return nd.child2 <= nd.child1; }   // scen
 
 }  // namespace
 
+// Device state of one in-flight pass: its own stream, ray state, reorder buffers and queues.
+struct PassCtx {
+    hipStream_t stream = nullptr;
+    DevBuf<float4> rays;
+    DevBuf<uint32_t> idx[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
+    DevBuf<uint8_t> bkt[2];
+    DevBuf<float2> hits;
+    DevBuf<float> psum;               // this pass's per-pixel sums (when the caller gives no buffer)
+    hipEvent_t fb_done = nullptr;     // recorded after this context last added into the framebuffer
+    hipEvent_t done = nullptr;
+    std::vector<hipEvent_t> events;   // (begin, end) pairs: process launches, then reorder launches
+    size_t ev = 0;
+
+    ~PassCtx() {
+        for (auto e : events) (void)hipEventDestroy(e);
+        if (fb_done) (void)hipEventDestroy(fb_done);
+        if (done) (void)hipEventDestroy(done);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    hipEvent_t event() {
+        if (ev == events.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            events.push_back(e);
+        }
+        return events[ev++];
+    }
+};
+
 struct rt_renderer {
     int device = 0;
-    hipStream_t stream = nullptr;
     bool sort = true, counters = false;
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
-    DevBuf<float4> spheres, tris, mats, nodes, rays;
+    DevBuf<float4> spheres, tris, mats, nodes;
     DevBuf<uint16_t> mat_idx;
     DevBuf<int2> big;
     DevBuf<float> env, fb;
-    DevBuf<uint32_t> idx[2], sort_counts, sort_offsets, sort_totals, live, queue;
-    DevBuf<float2> hits;
-    DevBuf<uint32_t> overflow;        // traversal stack overflow, 2 x (kStackMax - kStackLds) words per lane
-    DevBuf<uint8_t> bkt[2];
     DevBuf<Counters> ctr;
-    std::vector<hipEvent_t> events;
-    int resident_blocks = 0;          // trace_kernel workgroups resident on the whole chip
+    PassCtx ctx[kInflight];
+    int trace_blocks = 0;             // persistent trace_kernel grid
     int cus = 0;
     hipEvent_t t_begin = nullptr, t_end = nullptr;
 
     ~rt_renderer() {
-        for (auto e : events) (void)hipEventDestroy(e);
         if (t_begin) (void)hipEventDestroy(t_begin);
         if (t_end) (void)hipEventDestroy(t_end);
-        if (stream) (void)hipStreamDestroy(stream);
     }
 
+    hipStream_t stream() const { return ctx[0].stream; }
     int pass_count() const { return (spp + 19) / 20; }
 
     int init(const rt_scene *sc, const rt_opts *o) {
@@ -636,9 +661,14 @@ struct rt_renderer {
         spp = sc->ray_count;
         bounces = sc->bounces;
         HIPCHK(hipSetDevice(device));
-        HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        for (auto &c : ctx) {
+            HIPCHK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&c.fb_done, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
+        }
         HIPCHK(hipEventCreate(&t_begin));
         HIPCHK(hipEventCreate(&t_end));
+        hipStream_t s0 = stream();
         int rc;
         // Child-pair node records (see file header).  Internal nodes keep the reference's
         // depth-first order, so a subtree's records stay contiguous.
@@ -673,40 +703,45 @@ struct rt_renderer {
         }
         ds.root_ref = nn > 0 ? ref_of(0) : (kLeaf | 0u);
         if (big_h.empty()) big_h.push_back(make_int2(0, 0));
-        if ((rc = spheres.upload(sc->spheres, sc->sphere_count, stream))) return rc;
-        if ((rc = tris.upload(sc->triangles, (size_t)sc->triangle_count * 3, stream))) return rc;
-        if ((rc = mats.upload(sc->materials, (size_t)sc->material_count * 3, stream))) return rc;
-        if ((rc = mat_idx.upload(sc->material_indices, (size_t)sc->sphere_count + sc->triangle_count, stream))) return rc;
-        if ((rc = nodes.upload(rec_h.data(), rec_h.size(), stream))) return rc;
-        if ((rc = big.upload(big_h.data(), big_h.size(), stream))) return rc;
-        if ((rc = env.upload(sc->environment_map, (size_t)sc->environment_map_width * sc->environment_map_height * 3, stream)))
+        if ((rc = spheres.upload(sc->spheres, sc->sphere_count, s0))) return rc;
+        if ((rc = tris.upload(sc->triangles, (size_t)sc->triangle_count * 3, s0))) return rc;
+        if ((rc = mats.upload(sc->materials, (size_t)sc->material_count * 3, s0))) return rc;
+        if ((rc = mat_idx.upload(sc->material_indices, (size_t)sc->sphere_count + sc->triangle_count, s0))) return rc;
+        if ((rc = nodes.upload(rec_h.data(), rec_h.size(), s0))) return rc;
+        if ((rc = big.upload(big_h.data(), big_h.size(), s0))) return rc;
+        if ((rc = env.upload(sc->environment_map, (size_t)sc->environment_map_width * sc->environment_map_height * 3, s0)))
             return rc;
         const int64_t pixels = (int64_t)width * height;
-        const int64_t max_rays = pixels * 20;
+        const int64_t max_rays = pixels * std::min(20, std::max(1, spp));
         if (max_rays > 0x7fffffff / 3) return rtamd::fail(RT_E_INVALID, "image too large for 32-bit ray indices");
         if ((rc = fb.alloc((size_t)pixels * 3))) return rc;
-        if ((rc = rays.alloc((size_t)max_rays * 3))) return rc;
-        for (int k = 0; k < 2; k++) {
-            if ((rc = idx[k].alloc((size_t)max_rays))) return rc;
-            if ((rc = bkt[k].alloc((size_t)max_rays))) return rc;
-            if (!sort) break;
-        }
-        const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
-        if (sort) {
-            if ((rc = sort_counts.alloc((size_t)kBuckets * tiles))) return rc;
-            if ((rc = sort_offsets.alloc((size_t)kBuckets * tiles))) return rc;
-            if ((rc = sort_totals.alloc(kBuckets))) return rc;
-        }
         if ((rc = ctr.alloc(kCtrSlots))) return rc;
-        if ((rc = live.alloc((size_t)bounces + 1))) return rc;
-        if ((rc = queue.alloc((size_t)(bounces + 1) * kQueues * kQueueStride))) return rc;
-        if ((rc = hits.alloc((size_t)max_rays))) return rc;
         int per_cu = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<true, false>, kBlock, 0));
-        resident_blocks = std::max(1, cus * std::max(1, per_cu));
-        if ((rc = overflow.alloc((size_t)resident_blocks * kBlock * 2 * (kStackMax - kStackLds)))) return rc;
-        HIPCHK(hipMemsetAsync(fb.p, 0, fb.n * sizeof(float), stream));
+        trace_blocks = std::max(1, cus * std::max(1, per_cu) * kTraceOccPct / 100);
+        const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
+        const int inflight = std::min(kInflight, std::max(1, pass_count()));
+        for (int k = 0; k < inflight; k++) {
+            PassCtx &c = ctx[k];
+            if ((rc = c.rays.alloc((size_t)max_rays * 3))) return rc;
+            for (int q = 0; q < 2; q++) {
+                if ((rc = c.idx[q].alloc((size_t)max_rays))) return rc;
+                if ((rc = c.bkt[q].alloc((size_t)max_rays))) return rc;
+                if (!sort) break;
+            }
+            if (sort) {
+                if ((rc = c.sort_counts.alloc((size_t)kBuckets * tiles))) return rc;
+                if ((rc = c.sort_offsets.alloc((size_t)kBuckets * tiles))) return rc;
+                if ((rc = c.sort_totals.alloc(kBuckets))) return rc;
+            }
+            if ((rc = c.live.alloc((size_t)bounces + 1))) return rc;
+            if ((rc = c.queue.alloc((size_t)(bounces + 1) * kQueues * kQueueStride))) return rc;
+            if ((rc = c.hits.alloc((size_t)max_rays))) return rc;
+            if ((rc = c.overflow.alloc((size_t)trace_blocks * kBlock * 2 * (kStackMax - kStackLds)))) return rc;
+            if ((rc = c.psum.alloc((size_t)pixels * 3))) return rc;
+        }
+        HIPCHK(hipMemsetAsync(fb.p, 0, fb.n * sizeof(float), s0));
         ds.spheres = spheres.p;
         ds.tris = tris.p;
         ds.mat_idx = mat_idx.p;
@@ -727,21 +762,13 @@ struct rt_renderer {
         ds.inv_dim = v3(sc->inv_dimensions.x, sc->inv_dimensions.y, sc->inv_dimensions.z);
         ds.inv_w = sc->inv_width;
         ds.inv_h = sc->inv_height;
-        HIPCHK(hipStreamSynchronize(stream));
+        HIPCHK(hipStreamSynchronize(s0));
         return RT_OK;
     }
 
-    hipEvent_t event(size_t k) {
-        while (events.size() <= k) {
-            hipEvent_t e;
-            if (hipEventCreate(&e) != hipSuccess) return nullptr;
-            events.push_back(e);
-        }
-        return events[k];
-    }
-
-    // Pass p of `while (remaining_rays)` (raytracing.cu:222-254).
-    int run_pass(int p, float *pass_out, size_t &ev, int64_t &sorted) {
+    // Pass p of `while (remaining_rays)` (raytracing.cu:222-254) on context c; the pass's
+    // per-pixel sums go to `sums` (W*H*3).
+    int enqueue_pass(PassCtx &c, int p, float *sums, int64_t &sorted) {
         const int before = spp - 20 * p;
         const int rtc = std::min(before, 20);
         const int remaining = before - rtc;
@@ -749,24 +776,26 @@ struct rt_renderer {
         const int n = (int)(rtc * pixels);
         const int grid = blocks_for(n);
         const int tiles = (n + kSortTile - 1) / kSortTile;
-        int cur = 0;
-        const int tgrid = std::min(grid, resident_blocks);
+        const int tgrid = std::min(grid, trace_blocks);
         const int sgrid = std::min(grid, cus * 8);
-        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, stream, live.p, (uint32_t)n, bounces + 1, queue.p);
-        hipLaunchKernelGGL(generate_kernel, dim3(grid), dim3(kBlock), 0, stream, ds, rays.p, idx[0].p, bkt[0].p, rtc, n,
-                           709579u * (uint32_t)remaining);
+        hipStream_t st = c.stream;
+        int cur = 0;
+        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1, c.queue.p);
+        hipLaunchKernelGGL(generate_kernel, dim3(grid), dim3(kBlock), 0, st, ds, c.rays.p, c.idx[0].p, c.bkt[0].p, rtc,
+                           n, 709579u * (uint32_t)remaining);
         for (int b = 0; b < bounces; b++) {
             const uint32_t seed_term = 279220567u * (uint32_t)(remaining * 20 + b);
-            hipEvent_t e0 = event(ev++), e1 = event(ev++);
+            hipEvent_t e0 = c.event(), e1 = c.event();
             if (!e0 || !e1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
-            HIPCHK(hipEventRecord(e0, stream));
-            const uint32_t *lv = live.p + b;
-#define RT_PROCESS(SORTED, COUNT)                                                                               \
-    do {                                                                                                        \
-        hipLaunchKernelGGL((trace_kernel<SORTED, COUNT>), dim3(tgrid), dim3(kBlock), 0, stream, ds, rays.p,      \
-                           idx[cur].p, bkt[cur].p, lv, queue.p + (size_t)b * kQueues * kQueueStride, hits.p, overflow.p, ctr.p);                 \
-        hipLaunchKernelGGL((shade_kernel<SORTED, COUNT>), dim3(sgrid), dim3(kBlock), 0, stream, ds, rays.p,      \
-                           idx[cur].p, bkt[cur].p, lv, hits.p, seed_term, ctr.p);                               \
+            HIPCHK(hipEventRecord(e0, st));
+            const uint32_t *lv = c.live.p + b;
+            uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
+#define RT_PROCESS(SORTED, COUNT)                                                                                \
+    do {                                                                                                         \
+        hipLaunchKernelGGL((trace_kernel<SORTED, COUNT>), dim3(tgrid), dim3(kBlock), 0, st, ds, c.rays.p,         \
+                           c.idx[cur].p, c.bkt[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                      \
+        hipLaunchKernelGGL((shade_kernel<SORTED, COUNT>), dim3(sgrid), dim3(kBlock), 0, st, ds, c.rays.p,         \
+                           c.idx[cur].p, c.bkt[cur].p, lv, c.hits.p, seed_term, ctr.p);                            \
     } while (0)
             if (sort) {
                 if (counters) RT_PROCESS(true, true); else RT_PROCESS(true, false);
@@ -775,29 +804,31 @@ struct rt_renderer {
             }
 #undef RT_PROCESS
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(e1, stream));
+            HIPCHK(hipEventRecord(e1, st));
             if (sort && b + 1 != bounces) {
-                hipEvent_t s0 = event(ev++), s1 = event(ev++);
+                hipEvent_t s0 = c.event(), s1 = c.event();
                 if (!s0 || !s1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
-                HIPCHK(hipEventRecord(s0, stream));
-                hipLaunchKernelGGL(sort_hist_kernel, dim3(tiles), dim3(kBlock), 0, stream, bkt[cur].p, lv, tiles,
-                                   sort_counts.p);
-                hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, stream, sort_counts.p, lv, tiles,
-                                   sort_offsets.p, sort_totals.p, live.p + b + 1);
-                hipLaunchKernelGGL(sort_scatter_kernel, dim3(tiles), dim3(kBlock), 0, stream, bkt[cur].p, idx[cur].p, lv,
-                                   tiles, sort_offsets.p, sort_totals.p, bkt[1 - cur].p, idx[1 - cur].p);
+                HIPCHK(hipEventRecord(s0, st));
+                hipLaunchKernelGGL(sort_hist_kernel, dim3(tiles), dim3(kBlock), 0, st, c.bkt[cur].p, lv, tiles,
+                                   c.sort_counts.p);
+                hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, lv, tiles,
+                                   c.sort_offsets.p, c.sort_totals.p, c.live.p + b + 1);
+                hipLaunchKernelGGL(sort_scatter_kernel, dim3(tiles), dim3(kBlock), 0, st, c.bkt[cur].p, c.idx[cur].p,
+                                   lv, tiles, c.sort_offsets.p, c.sort_totals.p, c.bkt[1 - cur].p, c.idx[1 - cur].p);
                 HIPCHK(hipGetLastError());
-                HIPCHK(hipEventRecord(s1, stream));
+                HIPCHK(hipEventRecord(s1, st));
                 cur = 1 - cur;
                 sorted += n;
             }
         }
-        hipLaunchKernelGGL(accumulate_kernel, dim3(blocks_for(pixels)), dim3(kBlock), 0, stream, fb.p, rays.p, rtc,
-                           (int)pixels, pass_out);
+        hipLaunchKernelGGL(accumulate_kernel, dim3(blocks_for(pixels)), dim3(kBlock), 0, st, c.rays.p, rtc,
+                           (int)pixels, sums);
         HIPCHK(hipGetLastError());
         return RT_OK;
     }
 
+    // Passes pass_begin + k*stride, k < count, kInflight at a time on separate streams; the
+    // framebuffer adds stay in pass order through cross-stream events.
     int run(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st) {
         const auto w0 = std::chrono::high_resolution_clock::now();
         HIPCHK(hipSetDevice(device));
@@ -806,19 +837,34 @@ struct rt_renderer {
         if (count < 0) count = pass_begin < P ? (P - pass_begin + stride - 1) / stride : 0;
         if (pass_begin < 0 || (count > 0 && pass_begin + (int64_t)(count - 1) * stride >= P))
             return rtamd::fail(RT_E_INVALID, "pass range outside the render");
-        HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, stream));
-        HIPCHK(hipEventRecord(t_begin, stream));
-        size_t ev = 0;
+        const int inflight = std::min(kInflight, std::max(1, P));
+        hipStream_t s0 = stream();
+        HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, s0));
+        HIPCHK(hipEventRecord(t_begin, s0));
+        for (int k = 1; k < inflight; k++) HIPCHK(hipStreamWaitEvent(ctx[k].stream, t_begin, 0));
+        for (auto &c : ctx) c.ev = 0;
         int64_t sorted = 0, generated = 0;
-        const int64_t pixels = (int64_t)width * height;
+        const int64_t px3 = (int64_t)width * height * 3;
+        hipEvent_t prev_fb = nullptr;
         for (int k = 0; k < count; k++) {
+            PassCtx &c = ctx[k % inflight];
             const int p = pass_begin + k * stride;
-            const int rc = run_pass(p, pass_sums ? pass_sums + (size_t)k * pixels * 3 : nullptr, ev, sorted);
+            float *sums = pass_sums ? pass_sums + (size_t)k * px3 : c.psum.p;
+            const int rc = enqueue_pass(c, p, sums, sorted);
             if (rc) return rc;
-            generated += (int64_t)std::min(spp - 20 * p, 20) * pixels;
+            if (prev_fb) HIPCHK(hipStreamWaitEvent(c.stream, prev_fb, 0));
+            hipLaunchKernelGGL(add_kernel, dim3(blocks_for(px3)), dim3(kBlock), 0, c.stream, fb.p, sums, (int)px3);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(c.fb_done, c.stream));
+            prev_fb = c.fb_done;
+            generated += (int64_t)std::min(spp - 20 * p, 20) * width * height;
         }
-        HIPCHK(hipEventRecord(t_end, stream));
-        HIPCHK(hipStreamSynchronize(stream));
+        for (int k = 1; k < inflight; k++) {
+            HIPCHK(hipEventRecord(ctx[k].done, ctx[k].stream));
+            HIPCHK(hipStreamWaitEvent(s0, ctx[k].done, 0));
+        }
+        HIPCHK(hipEventRecord(t_end, s0));
+        HIPCHK(hipStreamSynchronize(s0));
         if (st) {
             std::memset(st, 0, sizeof(*st));
             std::vector<Counters> slots(kCtrSlots);
@@ -831,20 +877,24 @@ struct rt_renderer {
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, t_begin, t_end));
             st->kernel_ms = ms;
-            // Events come in (process begin, end) pairs, with (sort begin, end) pairs between.
+            // Per context, events come in (process begin, end) pairs with (reorder begin, end)
+            // pairs between them, in enqueue order.
             double proc = 0, srt = 0;
-            size_t k = 0;
-            for (int q = 0; q < count; q++)
-                for (int b = 0; b < bounces; b++) {
-                    HIPCHK(hipEventElapsedTime(&ms, events[k], events[k + 1]));
-                    proc += ms;
-                    k += 2;
-                    if (sort && b + 1 != bounces) {
-                        HIPCHK(hipEventElapsedTime(&ms, events[k], events[k + 1]));
-                        srt += ms;
-                        k += 2;
+            for (int q = 0; q < inflight; q++) {
+                const int passes_here = count > q ? (count - q + inflight - 1) / inflight : 0;
+                size_t e = 0;
+                for (int r = 0; r < passes_here; r++)
+                    for (int b = 0; b < bounces; b++) {
+                        HIPCHK(hipEventElapsedTime(&ms, ctx[q].events[e], ctx[q].events[e + 1]));
+                        proc += ms;
+                        e += 2;
+                        if (sort && b + 1 != bounces) {
+                            HIPCHK(hipEventElapsedTime(&ms, ctx[q].events[e], ctx[q].events[e + 1]));
+                            srt += ms;
+                            e += 2;
+                        }
                     }
-                }
+            }
             st->process_ms = proc;
             st->sort_ms = srt;
             st->generated_rays = (uint64_t)generated;
@@ -937,19 +987,35 @@ int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t s
     return r->run(pass_begin, count, stride, d_pass_sums, stats);
 }
 
+int rt_renderer_run_host(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride, float *host_pass_sums,
+                         rt_stats *stats) {
+    if (!r || !host_pass_sums || count < 1) return rtamd::fail(RT_E_INVALID, "rt_renderer_run_host: bad argument");
+    HIPCHK(hipSetDevice(r->device));
+    const size_t bytes = (size_t)count * r->width * r->height * 3 * sizeof(float);
+    float *d = nullptr;
+    HIPCHK(hipMalloc(reinterpret_cast<void **>(&d), bytes));
+    int rc = r->run(pass_begin, count, stride, d, stats);
+    if (!rc) {
+        const hipError_t e = hipMemcpy(host_pass_sums, d, bytes, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = hip_fail(e, "hipMemcpy pass sums");
+    }
+    (void)hipFree(d);
+    return rc;
+}
+
 int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out) {
     if (!r || !fb_out) return rtamd::fail(RT_E_INVALID, "null argument");
     HIPCHK(hipSetDevice(r->device));
-    HIPCHK(hipMemcpyAsync(fb_out, r->fb.p, r->fb.n * sizeof(float), hipMemcpyDeviceToHost, r->stream));
-    HIPCHK(hipStreamSynchronize(r->stream));
+    HIPCHK(hipMemcpyAsync(fb_out, r->fb.p, r->fb.n * sizeof(float), hipMemcpyDeviceToHost, r->stream()));
+    HIPCHK(hipStreamSynchronize(r->stream()));
     return RT_OK;
 }
 
 int rt_renderer_clear(rt_renderer *r) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
     HIPCHK(hipSetDevice(r->device));
-    HIPCHK(hipMemsetAsync(r->fb.p, 0, r->fb.n * sizeof(float), r->stream));
-    HIPCHK(hipStreamSynchronize(r->stream));
+    HIPCHK(hipMemsetAsync(r->fb.p, 0, r->fb.n * sizeof(float), r->stream()));
+    HIPCHK(hipStreamSynchronize(r->stream()));
     return RT_OK;
 }
 

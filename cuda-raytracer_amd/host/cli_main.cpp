@@ -53,18 +53,9 @@ int render_multi(const rt_scene *s, int sort, int ndev, std::vector<float> &fb, 
             rt_renderer *ren = nullptr;
             r.rc = rt_renderer_create(s, &o, &ren);
             if (r.rc) { r.err = rt_last_error(); return; }
-            // Pass sums are written to a device staging buffer by the renderer, one pass per call.
+            // All of this device's passes in one call (several in flight), sums back to the host.
             r.sums.assign((size_t)count * px3, 0.0f);
-            for (int q = 0; q < count && !r.rc; q++) {
-                r.rc = rt_renderer_clear(ren);
-                rt_stats st;
-                if (!r.rc) r.rc = rt_renderer_run(ren, k + q * ndev, 1, 1, nullptr, &st);
-                if (!r.rc) r.rc = rt_renderer_read_framebuffer(ren, r.sums.data() + (size_t)q * px3);
-                r.stats.live_segments += st.live_segments;
-                r.stats.generated_rays += st.generated_rays;
-                r.stats.kernel_ms += st.kernel_ms;
-                r.stats.process_ms += st.process_ms;
-            }
+            r.rc = rt_renderer_run_host(ren, k, count, ndev, r.sums.data(), &r.stats);
             if (r.rc) r.err = rt_last_error();
             rt_renderer_destroy(ren);
         });
@@ -88,6 +79,8 @@ int render_multi(const rt_scene *s, int sort, int ndev, std::vector<float> &fb, 
 }  // namespace
 
 int main(int argc, char **argv) {
+    // 4 passes in flight per device on 4 streams: give HIP enough hardware queues (read at init).
+    if (const char *q = std::getenv("GPU_MAX_HW_QUEUES"); !q || std::atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
     if (argc < 2) {
         std::printf("Usage: %s <scene>\n", argv[0]);
         return 1;

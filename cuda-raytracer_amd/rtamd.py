@@ -97,6 +97,7 @@ def lib():
         L.rt_render.argtypes = [P, P, P, P]
         L.rt_renderer_create.argtypes = [P, P, C.POINTER(P)]
         L.rt_renderer_run.argtypes = [P, I32, I32, I32, P, P]
+        L.rt_renderer_run_host.argtypes = [P, I32, I32, I32, P, P]
         L.rt_renderer_read_framebuffer.argtypes = [P, P]
         L.rt_renderer_clear.argtypes = [P]
         L.rt_renderer_set_counters.argtypes = [P, I32]
@@ -231,6 +232,13 @@ class Renderer:
         _check(lib().rt_renderer_run(self.h, pass_begin, count, stride,
                                      P(d_pass_sums) if d_pass_sums else None, C.byref(st)))
         return st.as_dict()
+
+    def run_host(self, pass_begin=0, count=1, stride=1):
+        """Renders passes and returns their per-pass sums (count, W*H*3) in host memory."""
+        out = np.zeros((count, self.scene.pixels * 3), np.float32)
+        st = RtStats()
+        _check(lib().rt_renderer_run_host(self.h, pass_begin, count, stride, _ptr(out), C.byref(st)))
+        return out, st.as_dict()
 
     def set_counters(self, on):
         _check(lib().rt_renderer_set_counters(self.h, int(on)))

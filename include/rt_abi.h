@@ -127,8 +127,10 @@ int rt_device_count(void);
  * framebuffer (W*H*3 floats, raw radiance sums, caller-owned) to fb_out. */
 int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stats *stats);
 
-/* Persistent renderer: scene resident in HBM, ray buffers sized for 20 rays/pixel.
- * Used by the benchmark and by the multi-GPU pass-sharded driver. */
+/* Persistent renderer: scene resident in HBM, ray buffers sized for 20 rays/pixel per pass,
+ * up to 4 passes in flight on separate streams (each with its own buffer set) so one pass's
+ * latency-bound last bounces overlap another's throughput-bound first bounces.  The framebuffer
+ * adds stay in pass order.  Used by rt_render, the benchmark and the multi-GPU drivers. */
 typedef struct rt_renderer rt_renderer;
 int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer **out);
 /* Renders passes pass_begin, pass_begin+stride, ... (count passes) and adds each pass's
@@ -137,6 +139,9 @@ int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer *
  * also stored there.  Blocking. */
 int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride,
                     float *d_pass_sums, rt_stats *stats);
+/* Same, with the per-pass sums returned in host memory (count*W*H*3 floats). */
+int rt_renderer_run_host(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride,
+                         float *host_pass_sums, rt_stats *stats);
 int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out);   /* device fb -> host     */
 int rt_renderer_clear(rt_renderer *r);                               /* zero the device fb    */
 int rt_renderer_set_counters(rt_renderer *r, int32_t enable);

@@ -115,3 +115,26 @@ def test_cli_multi_device_equals_single(gpu, tmp_path):
                        capture_output=True)
     assert a.returncode == 0 and b.returncode == 0
     assert open(tmp_path / "a.png", "rb").read() == open(tmp_path / "b.png", "rb").read()
+
+
+def test_many_passes_in_flight_bitexact(gpu):
+    """10 passes (4 in flight on separate streams): the ordered framebuffer adds must reproduce
+    the oracle's pass-ordered sum exactly, for sort on and off."""
+    image = (40, 32, 190, 5)                     # 10 passes, the last one 10 spp
+    for sort in (True, False):
+        osc, psc = _pair("cornell_plus", image)
+        ofb, ost = osc.render(sort=sort)
+        gfb, gst = R.render(psc, sort=sort)
+        assert np.array_equal(gfb, ofb), _diff(gfb, ofb)
+        assert gst["live_segments"] == ost["live_segments"]
+
+
+def test_run_host_pass_sums(gpu):
+    image = (32, 32, 100, 4)
+    osc, psc = _pair("cornell", image)
+    want = osc.pass_sums(sort=True, pass_begin=1, pass_count=2)
+    r = R.Renderer(psc, sort=True)
+    sums, st = r.run_host(pass_begin=1, count=2, stride=2)      # passes 1 and 3
+    assert np.array_equal(sums[0], want[0])
+    assert np.array_equal(sums[1], osc.pass_sums(sort=True, pass_begin=3, pass_count=1)[0])
+    r.close()

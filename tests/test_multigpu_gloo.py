@@ -30,10 +30,11 @@ def _worker(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sc = O.OracleScene(os.path.join(O.ASSETS, "cornell_plus.scene"), image=IMAGE)
 
-    def render_pass(p, out):
-        out.copy_(torch.from_numpy(sc.pass_sums(sort=True, pass_begin=p, pass_count=1, threads=2)[0]))
+    def render_passes(passes, out):
+        for j, p in enumerate(passes):
+            out[j].copy_(torch.from_numpy(sc.pass_sums(sort=True, pass_begin=p, pass_count=1, threads=2)[0]))
 
-    frame = D.PassShardedFrame(dist, torch, sc.pixels * 3, sc.passes, "cpu", render_pass)
+    frame = D.PassShardedFrame(dist, torch, sc.pixels * 3, sc.passes, "cpu", render_passes, max_rounds_per_call=2)
     n = frame.run_all()
     assert n == len(D.pass_schedule(rank, world, sc.passes))
     if rank == 0:
