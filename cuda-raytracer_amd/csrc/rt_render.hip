@@ -106,24 +106,22 @@ __device__ __forceinline__ uint32_t rank_below(unsigned long long mask) {
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // ---------------------------------------------------------------- ray generation
-// scene.cu:78-105 + raytracing.cu:76-81.  Ray layout: 3 x float4 = origin, dir, T, C.
-__global__ __launch_bounds__(kBlock) void generate_kernel(DevScene S, float4 *__restrict__ rays,
-                                                          uint32_t *__restrict__ idx, uint8_t *__restrict__ bkt,
-                                                          int rtc, int n, uint32_t seed_term) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    Rng rng = pcg_seed((uint32_t)i * 0x85810BEAu + seed_term);   // 298592570346 mod 2^32
-    const int pixel = i / rtc;
+// generate_initial_rays (scene.cu:78-105, raytracing.cu:76-81), evaluated where a bounce-0 ray
+// is needed (trace and shade of bounce 0) instead of being written out and read back.  Ray i
+// of a pass is slot i at bounce 0.  Ray state afterwards: geo[2 i .. 2 i + 1] = {o.xyz, d.x},
+// {d.yz, T.xy} (what traversal reads) and tc[i] = {T.z, C.xyz} (what accumulation reads).
+struct PassArgs {
+    int rtc;                          // rays per pixel this pass
+    uint32_t gen_seed_term;           // 709579 * remaining (scene.cu:81)
+};
+
+__device__ __forceinline__ V3 primary_dir(const DevScene &S, int i, const PassArgs &pa) {
+    Rng rng = pcg_seed((uint32_t)i * 0x85810BEAu + pa.gen_seed_term);   // 298592570346 mod 2^32
+    const int pixel = i / pa.rtc;
     const int x = pixel % S.width, y = pixel / S.width;
-    idx[i] = (uint32_t)i;
-    bkt[i] = 0;
     const float xc = (x + random01(rng)) * S.inv_w;
     const float yc = (y + random01(rng)) * S.inv_h;
-    const V3 d = normalise(S.tl + xc * S.sr - yc * S.su);
-    float4 *r = rays + (size_t)i * 3;
-    r[0] = make_float4(S.cam.x, S.cam.y, S.cam.z, d.x);
-    r[1] = make_float4(d.y, d.z, 1.0f, 1.0f);
-    r[2] = make_float4(1.0f, 0.0f, 0.0f, 0.0f);
+    return normalise(S.tl + xc * S.sr - yc * S.su);
 }
 
 // ---------------------------------------------------------------- traversal
@@ -132,8 +130,8 @@ __global__ __launch_bounds__(kBlock) void generate_kernel(DevScene S, float4 *__
 // chunks of slots from a device queue (one atomic per chunk) and hands a new slot to a lane
 // as soon as that lane's ray is done, so incoherent rays of very different traversal lengths
 // do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
-template <bool SORTED, bool COUNT>
-__global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, const float4 *__restrict__ rays,
+template <bool SORTED, bool COUNT, bool FIRST>
+__global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ idx,
                                                        const uint8_t *__restrict__ bkt,
                                                        const uint32_t *__restrict__ live_count,
@@ -191,14 +189,20 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, const float4 
                 idle &= ~took;
             }
             if (fresh) {
-                if (!SORTED && bkt[slot] == kDead) {
+                if (!FIRST && !SORTED && bkt[slot] == kDead) {
                     slot = -1;          // no_sort: terminated rays stay in place
                 } else {
                     nlive++;
-                    const float4 *rp = rays + (size_t)(SORTED ? idx[slot] : (uint32_t)slot) * 3;
-                    const float4 r0 = rp[0], r1 = rp[1];
-                    o = v3(r0.x, r0.y, r0.z);
-                    d = v3(r0.w, r1.x, r1.y);
+                    if (FIRST) {
+                        o = S.cam;
+                        d = primary_dir(S, slot, pa);
+                    } else {
+                        const float4 *rp = geo + (size_t)(SORTED ? idx[slot] : (uint32_t)slot) * 2;
+                        const float4 r0 = rp[0];
+                        const float2 r1 = *reinterpret_cast<const float2 *>(rp + 1);
+                        o = v3(r0.x, r0.y, r0.z);
+                        d = v3(r0.w, r1.x, r1.y);
+                    }
                     ix = 1 / d.x; iy = 1 / d.y; iz = 1 / d.z;
                     closest = 1e30f;
                     index = -1;
@@ -318,25 +322,42 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, const float4 
 
 // Shading for the live slots (scene.cu:376-485): environment lookup on a miss, otherwise
 // emission + scatter; then the new ray state and its reorder bucket.  One lane per slot.
-template <bool SORTED, bool COUNT>
-__global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, float4 *__restrict__ rays,
-                                                       const uint32_t *__restrict__ idx, uint8_t *__restrict__ bkt,
-                                                       const uint32_t *__restrict__ live_count,
+template <bool SORTED, bool COUNT, bool FIRST>
+__global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
+                                                       float4 *__restrict__ tc, uint32_t *__restrict__ idx,
+                                                       uint8_t *__restrict__ bkt, const uint32_t *__restrict__ live_count,
                                                        const float2 *__restrict__ hits, uint32_t seed_term,
                                                        Counters *__restrict__ ctr) {
     const int L = (int)__builtin_amdgcn_readfirstlane(*live_count);
     unsigned hit = 0, miss = 0, hit_sphere = 0;
     for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
         const int slot = base + threadIdx.x;
-        if (slot >= L || bkt[slot] == kDead) continue;
+        if (slot >= L || (!FIRST && bkt[slot] == kDead)) continue;
         Rng rng = pcg_seed((uint32_t)slot * 4137874753u + seed_term);   // raytracing.cu:89
         const float2 h = hits[slot];
         const float closest = h.x;
         const int index = __float_as_int(h.y);
-        float4 *rp = rays + (size_t)(SORTED ? idx[slot] : (uint32_t)slot) * 3;
-        const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
-        const V3 o = v3(r0.x, r0.y, r0.z), d = v3(r0.w, r1.x, r1.y);
-        V3 T = v3(r1.z, r1.w, r2.x), C = v3(r2.y, r2.z, r2.w);
+        const uint32_t ri = (SORTED && !FIRST) ? idx[slot] : (uint32_t)slot;
+        V3 o, d, T, C;
+        if (FIRST) {
+            o = S.cam;
+            d = primary_dir(S, slot, pa);
+            // T is laundered through an empty asm: with T a compile-time (1,1,1) the gfx950
+            // backend dropped T.xy on the dielectric-reflect path of scatter (ROCm 7.2 clang;
+            // T.xy came out as stale registers while T.z was right).  Keeping T opaque gives the
+            // same code shape as bounces >= 1, which is parity-clean.
+            float tx = 1.f, ty = 1.f, tz = 1.f;
+            asm volatile("" : "+v"(tx), "+v"(ty), "+v"(tz));
+            T = v3(tx, ty, tz);
+            C = v3(0, 0, 0);
+            if (SORTED) idx[slot] = (uint32_t)slot;
+        } else {
+            const float4 r0 = geo[(size_t)ri * 2], r1 = geo[(size_t)ri * 2 + 1], r2 = tc[ri];
+            o = v3(r0.x, r0.y, r0.z);
+            d = v3(r0.w, r1.x, r1.y);
+            T = v3(r1.z, r1.w, r2.x);
+            C = v3(r2.y, r2.z, r2.w);
+        }
         V3 no = o, nd = d;
         if (index == -1) {
             miss++;
@@ -356,9 +377,9 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, float4 *__res
             }
             scatter(d, normal, load_mat(S.mats + (size_t)S.mat_idx[index] * 3), rng, T, C, nd);
         }
-        rp[0] = make_float4(no.x, no.y, no.z, nd.x);
-        rp[1] = make_float4(nd.y, nd.z, T.x, T.y);
-        rp[2] = make_float4(T.z, C.x, C.y, C.z);
+        geo[(size_t)ri * 2] = make_float4(no.x, no.y, no.z, nd.x);
+        geo[(size_t)ri * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
+        tc[ri] = make_float4(T.z, C.x, C.y, C.z);
         bkt[slot] = (uint8_t)(is_black(T) ? kDead : bucket_of(no, nd, S.min_coord, S.inv_dim));
     }
     if (COUNT) {
@@ -505,14 +526,14 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
 // ---------------------------------------------------------------- accumulate
 // Ordered per-pixel sum of the pass's samples (the caller then adds it: fb += sum, in pass order) (raytracing.cu:96-107 without
 // the unordered atomics; the CPU path's order, raytracing.cu:114-120).
-__global__ __launch_bounds__(kBlock) void accumulate_kernel(const float4 *__restrict__ rays, int rtc, int pixels,
+__global__ __launch_bounds__(kBlock) void accumulate_kernel(const float4 *__restrict__ tc, int rtc, int pixels,
                                                             float *__restrict__ sums) {
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p >= pixels) return;
     float sx = 0, sy = 0, sz = 0;
-    const float4 *r = rays + (size_t)p * rtc * 3 + 2;
+    const float4 *r = tc + (size_t)p * rtc;
     for (int s = 0; s < rtc; s++) {
-        const float4 c = r[(size_t)s * 3];
+        const float4 c = r[s];
         sx = sx + c.y;
         sy = sy + c.z;
         sz = sz + c.w;
@@ -603,7 +624,7 @@ bool is_leaf(const rt_bvh_node &nd) { return nd.child2 <= nd.child1; }   // scen
 // Device state of one in-flight pass: its own stream, ray state, reorder buffers and queues.
 struct PassCtx {
     hipStream_t stream = nullptr;
-    DevBuf<float4> rays;
+    DevBuf<float4> geo, tc;           // ray state by ray index: 2 x float4 traversal part, {T.z, C}
     DevBuf<uint32_t> idx[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
     DevBuf<uint8_t> bkt[2];
     DevBuf<float2> hits;
@@ -718,13 +739,14 @@ struct rt_renderer {
         if ((rc = ctr.alloc(kCtrSlots))) return rc;
         int per_cu = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<true, false>, kBlock, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<true, false, false>, kBlock, 0));
         trace_blocks = std::max(1, cus * std::max(1, per_cu) * kTraceOccPct / 100);
         const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
         const int inflight = std::min(kInflight, std::max(1, pass_count()));
         for (int k = 0; k < inflight; k++) {
             PassCtx &c = ctx[k];
-            if ((rc = c.rays.alloc((size_t)max_rays * 3))) return rc;
+            if ((rc = c.geo.alloc((size_t)max_rays * 2))) return rc;
+            if ((rc = c.tc.alloc((size_t)max_rays))) return rc;
             for (int q = 0; q < 2; q++) {
                 if ((rc = c.idx[q].alloc((size_t)max_rays))) return rc;
                 if ((rc = c.bkt[q].alloc((size_t)max_rays))) return rc;
@@ -781,8 +803,7 @@ struct rt_renderer {
         hipStream_t st = c.stream;
         int cur = 0;
         hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1, c.queue.p);
-        hipLaunchKernelGGL(generate_kernel, dim3(grid), dim3(kBlock), 0, st, ds, c.rays.p, c.idx[0].p, c.bkt[0].p, rtc,
-                           n, 709579u * (uint32_t)remaining);
+        const PassArgs pa{rtc, 709579u * (uint32_t)remaining};
         for (int b = 0; b < bounces; b++) {
             const uint32_t seed_term = 279220567u * (uint32_t)(remaining * 20 + b);
             hipEvent_t e0 = c.event(), e1 = c.event();
@@ -790,12 +811,16 @@ struct rt_renderer {
             HIPCHK(hipEventRecord(e0, st));
             const uint32_t *lv = c.live.p + b;
             uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
+#define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
+    do {                                                                                                         \
+        hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,        \
+                           c.geo.p, c.idx[cur].p, c.bkt[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);              \
+        hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST>), dim3(sgrid), dim3(kBlock), 0, st, ds, pa,        \
+                           c.geo.p, c.tc.p, c.idx[cur].p, c.bkt[cur].p, lv, c.hits.p, seed_term, ctr.p);         \
+    } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
     do {                                                                                                         \
-        hipLaunchKernelGGL((trace_kernel<SORTED, COUNT>), dim3(tgrid), dim3(kBlock), 0, st, ds, c.rays.p,         \
-                           c.idx[cur].p, c.bkt[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                      \
-        hipLaunchKernelGGL((shade_kernel<SORTED, COUNT>), dim3(sgrid), dim3(kBlock), 0, st, ds, c.rays.p,         \
-                           c.idx[cur].p, c.bkt[cur].p, lv, c.hits.p, seed_term, ctr.p);                            \
+        if (b == 0) RT_PROCESS3(SORTED, COUNT, true); else RT_PROCESS3(SORTED, COUNT, false);                     \
     } while (0)
             if (sort) {
                 if (counters) RT_PROCESS(true, true); else RT_PROCESS(true, false);
@@ -803,6 +828,7 @@ struct rt_renderer {
                 if (counters) RT_PROCESS(false, true); else RT_PROCESS(false, false);
             }
 #undef RT_PROCESS
+#undef RT_PROCESS3
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(e1, st));
             if (sort && b + 1 != bounces) {
@@ -821,8 +847,13 @@ struct rt_renderer {
                 sorted += n;
             }
         }
-        hipLaunchKernelGGL(accumulate_kernel, dim3(blocks_for(pixels)), dim3(kBlock), 0, st, c.rays.p, rtc,
-                           (int)pixels, sums);
+        if (bounces == 0) {
+            // rays were generated with collected = 0 and never processed (raytracing.cu:232)
+            HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
+        } else {
+            hipLaunchKernelGGL(accumulate_kernel, dim3(blocks_for(pixels)), dim3(kBlock), 0, st, c.tc.p, rtc,
+                               (int)pixels, sums);
+        }
         HIPCHK(hipGetLastError());
         return RT_OK;
     }

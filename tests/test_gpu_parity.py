@@ -24,6 +24,8 @@ CASES = [
     ("teapot", (96, 54, 20, 16), False, True),
     ("glass_teapot", (96, 54, 20, 16), True, True),
     ("lamp_available", (80, 45, 20, 32), True, True),
+    ("cornell", (16, 16, 3, 0), True, True),          # zero bounces: black image
+    ("spheres", (33, 17, 7, 1), False, True),         # odd sizes, one bounce, partial pass
 ]
 
 
