@@ -44,9 +44,6 @@ namespace {
 #ifndef RT_CHUNK_MAX
 #define RT_CHUNK_MAX 128
 #endif
-#ifndef RT_TRI_BATCH
-#define RT_TRI_BATCH 4
-#endif
 #ifndef RT_INFLIGHT
 #define RT_INFLIGHT 4
 #endif
@@ -66,7 +63,7 @@ constexpr int kCtrSlots = 64;       // striped copies of the work counters
 constexpr int kChunkMax = RT_CHUNK_MAX; // slots a wave takes from the trace queue per atomic...
 constexpr int kChunkMin = 64;        // ...shrunk so that every wave gets ~4 chunks when few rays live
 constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are idle
-constexpr int kTriBatch = RT_TRI_BATCH; // leaf triangles whose loads are issued together
+ // leaf triangles whose loads are issued together
 constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffer set each)
 constexpr int kTraceOccPct = RT_TRACE_OCC; // % of the resident trace workgroups the persistent grid uses
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
@@ -125,6 +122,17 @@ __device__ __forceinline__ V3 primary_dir(const DevScene &S, int i, const PassAr
 }
 
 // ---------------------------------------------------------------- traversal
+// Triangle range [ti, te) of a leaf ref (small leaves inline, big ones through big_leaves).
+__device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int &ti, int &te) {
+    if (ref & kBigLeaf) {
+        const int2 be = S.big_leaves[ref & 0x3FFFFFFFu];
+        ti = be.x; te = be.y;
+    } else {
+        ti = (int)(ref & 0xFFFFFFu);
+        te = ti + (int)((ref >> 24) & 0x3Fu);
+    }
+}
+
 // Closest hit for the live slots [0, *live): the sphere loop (scene.cu:338-372) and
 // bvh_closest_hit_distance (scene.cu:134-241).  Persistent and wave-refilling: each wave takes
 // chunks of slots from a device queue (one atomic per chunk) and hands a new slot to a lane
@@ -159,6 +167,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
     float ix = 0, iy = 0, iz = 0, closest = 0;
     int index = -1, sp = 0;
     uint32_t ref = 0;
+    int ti = 0, te = 0;                 // the lane is in a leaf while ti < te
     unsigned pn = 0, iv = 0, tt = 0, nlive = 0;
     while (true) {
         // ---- refill idle lanes (wave-uniform control flow)
@@ -213,6 +222,15 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
                     }
                     ref = S.root_ref;   // root is popped with distance 0 < closest
                     sp = 0;
+                    if (COUNT) pn++;
+                    ti = te = 0;
+                    if (ref & kLeaf) {
+                        leaf_range(S, ref, ti, te);
+                        if (ti == te) {  // no triangles at all: spheres only
+                            hits[slot] = make_float2(closest, __int_as_float(index));
+                            slot = -1;
+                        }
+                    }
                 }
             }
         }
@@ -221,10 +239,24 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
             continue;
         }
         if (slot < 0) continue;
-        // ---- one node visit
-        if (COUNT) pn++;
-        bool descend = false;
-        if (!(ref & kLeaf)) {
+        // ---- one step: a single triangle test of the current leaf, or one internal node
+        // (both children's slabs).  One triangle per step keeps the leaf branch as short as the
+        // internal one, so lanes at leaves and lanes at internal nodes share a step at ~50 %
+        // SIMD efficiency instead of the whole wave running a leaf's worth of triangle tests.
+        // The node/triangle visit order per lane is the reference's (scene.cu:145-238).
+        bool need = false;              // the lane needs the next node from its stack
+        if (ti < te) {
+            const float4 *tp = S.tris + (size_t)ti * 3;
+            const float4 q0 = tp[0], q1 = tp[1];
+            const float q2 = tp[2].x;
+            if (COUNT) tt++;
+            float t;
+            if (ray_triangle(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t)) {
+                closest = t;
+                index = S.sphere_count + ti;
+            }
+            need = ++ti == te;
+        } else {
             if (COUNT) iv++;
             const float4 *nd = S.nodes + (size_t)ref * 4;
             const float4 a = nd[0], b = nd[1], c = nd[2];
@@ -232,6 +264,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
             float t0, t1;
             const bool h0 = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, ix, iy, iz, closest, t0);
             const bool h1 = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, ix, iy, iz, closest, t1);
+            bool descend = false;
             if (h0 && h1) {
                 // The reference pushes near then far (scene.cu:204-225): the far child is next.
                 uint2 below;
@@ -253,56 +286,39 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
                 ref = kids.y;
                 descend = !(t1 >= closest);
             }
-        } else {
-            int begin, end;
-            if (ref & kBigLeaf) {
-                const int2 be = S.big_leaves[ref & 0x3FFFFFFFu];
-                begin = be.x; end = be.y;
-            } else {
-                begin = (int)(ref & 0xFFFFFFu);
-                end = begin + (int)((ref >> 24) & 0x3Fu);
-            }
-            for (int i = begin; i < end; i += kTriBatch) {   // Möller–Trumbore, scene.cu:160-195
-                // Issue the loads of up to kTriBatch triangles before testing them in order.
-                float4 q[kTriBatch][3];
-#pragma unroll
-                for (int k = 0; k < kTriBatch; k++) {
-                    const float4 *tp = S.tris + (size_t)min(i + k, end - 1) * 3;
-                    q[k][0] = tp[0]; q[k][1] = tp[1]; q[k][2] = tp[2];
-                }
-#pragma unroll
-                for (int k = 0; k < kTriBatch; k++) {
-                    if (i + k < end) {
-                        if (COUNT) tt++;
-                        float t;
-                        if (ray_triangle(o, d, v3(q[k][0].x, q[k][0].y, q[k][0].z), v3(q[k][0].w, q[k][1].x, q[k][1].y),
-                                         v3(q[k][1].z, q[k][1].w, q[k][2].x), closest, t)) {
-                            closest = t;
-                            index = S.sphere_count + i + k;
-                        }
-                    }
+            need = !descend;
+            if (descend) {
+                if (COUNT) pn++;
+                if (ref & kLeaf) {
+                    leaf_range(S, ref, ti, te);
+                    need = ti == te;
                 }
             }
         }
-        if (!descend) {
-            bool found = false;
-            while (sp > 0) {
-                sp--;
-                uint32_t eref;
-                float edist;
-                if (__builtin_expect(sp < kStackLds, 1)) {
-                    const uint2 e = col[sp * kBlock];
-                    eref = e.x;
-                    edist = __uint_as_float(e.y);
-                } else {
-                    eref = ovf_ref[(sp - kStackLds) * lanes];
-                    edist = ovf_dist[(sp - kStackLds) * lanes];
-                }
-                if (!(edist >= closest)) { ref = eref; found = true; break; }
-            }
-            if (!found) {
+        while (need) {                  // pop to the next entry nearer than closest
+            if (sp == 0) {
                 hits[slot] = make_float2(closest, __int_as_float(index));
                 slot = -1;
+                break;
+            }
+            sp--;
+            uint32_t eref;
+            float edist;
+            if (__builtin_expect(sp < kStackLds, 1)) {
+                const uint2 e = col[sp * kBlock];
+                eref = e.x;
+                edist = __uint_as_float(e.y);
+            } else {
+                eref = ovf_ref[(sp - kStackLds) * lanes];
+                edist = ovf_dist[(sp - kStackLds) * lanes];
+            }
+            if (edist >= closest) continue;
+            ref = eref;
+            if (COUNT) pn++;
+            need = false;
+            if (ref & kLeaf) {
+                leaf_range(S, ref, ti, te);
+                need = ti == te;
             }
         }
     }

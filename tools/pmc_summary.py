@@ -1,8 +1,11 @@
-"""Summarise tools/pmc.sh output per kernel and per bounce: HBM traffic (FETCH_SIZE doubled per
-MI355X_MICROARCH.md §HBM for wide streaming reads is NOT applied to gather traffic; both the raw
-and the corrected figure are printed), L2 hit rate, effective clock, wave stats.
+"""Summarise tools/pmc.sh output per kernel: every collected counter averaged per dispatch, plus
+derived figures (HBM-side bytes, L2 hit rate, VALU utilisation, TA busy).
 
-    python tools/pmc_summary.py TAG [bounces] [--json out.json --workload "..."]"""
+    python tools/pmc_summary.py TAG [TAG ...] [--json out.json --workload "..." --bounces 16]
+
+HBM-side bytes: FETCH_SIZE/WRITE_SIZE as reported, and the request-size-priced figure
+128*RDREQ_128B + 64*RDREQ_64B + 32*RDREQ_32B (MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE
+tallies 128-B requests at 64 B).  Both count Infinity-Cache hits (L2 -> fabric requests)."""
 import collections
 import csv
 import glob
@@ -19,61 +22,97 @@ def kname(n):
     return (m.group(1) + (m.group(2) or "").replace(" ", "")) if m else n[:30]
 
 
+def collect(tags):
+    """(kernel, k-th dispatch of that kernel in the run) -> {counter: value, dur_ms}."""
+    disp = collections.OrderedDict()
+    for tag in tags:
+        for path in sorted(glob.glob(os.path.join(REPO, "gpurun_out", "pmc_%s_*" % tag, "run_counter_collection.csv"))):
+            seen = collections.Counter()
+            last = None
+            for r in csv.DictReader(open(path)):
+                k = kname(r["Kernel_Name"])
+                did = r["Dispatch_Id"]
+                if (k, did) != last:
+                    seen[k] += 1
+                    last = (k, did)
+                d = disp.setdefault((k, seen[k]), {})
+                d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                d["dur_ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    return disp
+
+
+def derive(avg):
+    out = {}
+    if "FETCH_SIZE" in avg:
+        out["fetch_size_bytes"] = avg["FETCH_SIZE"] * 1024
+    if "WRITE_SIZE" in avg:
+        out["write_size_bytes"] = avg["WRITE_SIZE"] * 1024
+    if "TCC_EA0_RDREQ_128B_sum" in avg and "TCC_EA0_RDREQ_64B_sum" in avg:
+        n128, n64, n32 = avg["TCC_EA0_RDREQ_128B_sum"], avg["TCC_EA0_RDREQ_64B_sum"], avg.get("TCC_EA0_RDREQ_32B_sum", 0)
+        out["read_bytes_by_size"] = 128 * n128 + 64 * n64 + 32 * n32
+        if "TCC_EA0_RDREQ_sum" in avg:
+            out["rdreq_unclassified"] = avg["TCC_EA0_RDREQ_sum"] - n128 - n64 - n32
+    if "TCC_EA0_WRREQ_sum" in avg and "TCC_EA0_WRREQ_64B_sum" in avg:
+        n, n64 = avg["TCC_EA0_WRREQ_sum"], avg["TCC_EA0_WRREQ_64B_sum"]
+        out["write_bytes_by_size"] = 64 * n64 + 32 * (n - n64)
+    if avg.get("TCC_HIT_sum", 0) + avg.get("TCC_MISS_sum", 0):
+        out["l2_hit"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+    if avg.get("SQ_ACTIVE_INST_VALU") and avg.get("SQ_BUSY_CYCLES"):
+        out["valu_active_per_busy_cycle"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_BUSY_CYCLES"]
+    if avg.get("SQ_THREAD_CYCLES_VALU") and avg.get("SQ_ACTIVE_INST_VALU"):
+        out["valu_lane_util"] = avg["SQ_THREAD_CYCLES_VALU"] / (64 * avg["SQ_ACTIVE_INST_VALU"])
+    if avg.get("SQ_WAIT_INST_ANY") and avg.get("SQ_WAVE_CYCLES"):
+        out["wait_inst_frac"] = avg["SQ_WAIT_INST_ANY"] / avg["SQ_WAVE_CYCLES"]
+    if avg.get("SQ_WAVE_CYCLES") and avg.get("SQ_BUSY_CYCLES"):
+        out["avg_waves"] = avg["SQ_WAVE_CYCLES"] / avg["SQ_BUSY_CYCLES"]
+    if avg.get("TCP_TCC_READ_REQ_LATENCY_sum") and avg.get("TCP_TCC_READ_REQ_sum"):
+        out["l1_to_l2_read_latency_cycles"] = avg["TCP_TCC_READ_REQ_LATENCY_sum"] / avg["TCP_TCC_READ_REQ_sum"]
+    if avg.get("GRBM_GUI_ACTIVE"):
+        out["gpu_cycles"] = avg["GRBM_GUI_ACTIVE"]
+        if avg.get("TA_BUSY_avr"):
+            out["ta_busy_frac"] = avg["TA_BUSY_avr"] / avg["GRBM_GUI_ACTIVE"]
+    return out
+
+
 def main():
-    tag = sys.argv[1]
-    bounces = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 16
-    disp = collections.OrderedDict()     # (kernel, k-th dispatch) -> counters
-    for path in sorted(glob.glob(os.path.join(REPO, "gpurun_out", "pmc_%s_*" % tag, "run_counter_collection.csv"))):
-        seen = collections.Counter()
-        last = None
-        for r in csv.DictReader(open(path)):
-            k = kname(r["Kernel_Name"])
-            did = r["Dispatch_Id"]
-            if (k, did) != last:
-                seen[k] += 1
-                last = (k, did)
-            d = disp.setdefault((k, seen[k]), {})
-            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-            d["dur_ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    argv = sys.argv[1:]
+    opts = {}
+    for flag in ("--json", "--workload", "--bounces"):
+        if flag in argv:
+            i = argv.index(flag)
+            opts[flag] = argv[i + 1]
+            del argv[i:i + 2]
+    disp = collect(argv)
     per_kernel = collections.OrderedDict()
     for (k, i), d in disp.items():
         per_kernel.setdefault(k, []).append(d)
     summary = {}
     for k, ds in per_kernel.items():
-        tot = collections.Counter()
-        for d in ds:
-            tot.update(d)
-        n = len(ds)
-        fetch = tot.get("FETCH_SIZE", 0) * 1024
-        write = tot.get("WRITE_SIZE", 0) * 1024
-        hit, miss = tot.get("TCC_HIT_sum", 0), tot.get("TCC_MISS_sum", 0)
-        rd, dram = tot.get("TCC_EA0_RDREQ_sum", 0), tot.get("TCC_EA0_RDREQ_DRAM_sum", 0)
-        clk = tot.get("GRBM_GUI_ACTIVE", 0) / 8 / (tot["dur_ms"] / 1e3) / 1e9 if tot.get("GRBM_GUI_ACTIVE") else 0
-        summary[k] = dict(dispatches=n, fetch_bytes_per_dispatch=fetch / n, write_bytes_per_dispatch=write / n,
-                          l2_hit=hit / (hit + miss) if hit + miss else None,
-                          dram_rdreq_frac=dram / rd if rd else None, clock_ghz=clk)
-        print("%-28s n=%3d  FETCH %.3g B/disp  WRITE %.3g B/disp  L2 hit %s  EA rd->DRAM %s  clk %.2f GHz" % (
-            k, n, fetch / n, write / n, "%.3f" % (hit / (hit + miss)) if hit + miss else "-",
-            "%.3f" % (dram / rd) if rd else "-", clk))
-        if "trace_kernel" in k and n >= bounces:
-            for b in range(bounces):
-                d = ds[b]
-                print("   bounce %2d  %.3f ms  fetch %.3g  write %.3g  L2hit %s" % (
-                    b, d["dur_ms"], d.get("FETCH_SIZE", 0) * 1024, d.get("WRITE_SIZE", 0) * 1024,
-                    "%.3f" % (d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])) if d.get("TCC_HIT_sum") else "-"))
-    if "--json" in sys.argv:
-        out = sys.argv[sys.argv.index("--json") + 1]
-        wl = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else ""
-        tr, sh = summary.get("trace_kernel<true,false>"), summary.get("shade_kernel<true,false>")
-        rec = {"workload": wl, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/pmc.sh %s)" % tag,
-               "kernels": summary}
-        if tr and sh:
-            rec["hbm_bytes_per_launch"] = int(tr["fetch_bytes_per_dispatch"] + tr["write_bytes_per_dispatch"] +
-                                              sh["fetch_bytes_per_dispatch"] + sh["write_bytes_per_dispatch"])
-            rec["note"] = ("per process launch = one trace_kernel + one shade_kernel dispatch, averaged over the "
-                           "16 bounces of one pass; FETCH_SIZE/WRITE_SIZE as reported (KiB x 1024), no 2x gfx950 "
-                           "streaming correction applied (gather traffic, not wide streaming)")
-        json.dump(rec, open(out, "w"), indent=1)
+        keys = set().union(*ds)
+        avg = {c: sum(d.get(c, 0.0) for d in ds) / len(ds) for c in keys}
+        rec = {"dispatches": len(ds), "counters_per_dispatch": avg, "derived": derive(avg)}
+        summary[k] = rec
+        print("%-30s n=%3d %s" % (k, len(ds), "  ".join("%s=%.4g" % kv for kv in sorted(rec["derived"].items()))))
+    if "--json" in opts:
+        bounces = int(opts.get("--bounces", 16))
+        rec = {"workload": opts.get("--workload", ""), "source": "rocprofv3 --pmc, one pass per counter group "
+               "(tools/pmc.sh; tags %s)" % ",".join(argv), "kernels": summary}
+        proc = [k for k in summary if k.startswith("trace_kernel") or k.startswith("shade_kernel")]
+
+        def total(field):
+            return sum(summary[k]["derived"].get(field, 0) * summary[k]["dispatches"] for k in proc)
+        rd = total("read_bytes_by_size") or total("fetch_size_bytes")
+        wr = total("write_bytes_by_size") or total("write_size_bytes")
+        if proc and rd:
+            rec["hbm_bytes_per_launch"] = int((rd + wr) / bounces)
+            rec["hbm_read_bytes_per_launch"] = int(rd / bounces)
+            rec["hbm_write_bytes_per_launch"] = int(wr / bounces)
+            rec["fetch_size_bytes_per_launch"] = int(total("fetch_size_bytes") / bounces)
+            rec["note"] = ("per process launch = one trace_kernel + one shade_kernel dispatch (bounce 0 included), "
+                           "summed over the bounces of the profiled pass and divided by their number; reads priced by "
+                           "request size (TCC_EA0_RDREQ_{128B,64B,32B}), writes by TCC_EA0_WRREQ{,_64B}; L2->fabric "
+                           "requests, so Infinity-Cache hits are included (an upper bound on HBM bytes)")
+        json.dump(rec, open(opts["--json"], "w"), indent=1)
 
 
 if __name__ == "__main__":
