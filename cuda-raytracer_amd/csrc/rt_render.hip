@@ -63,7 +63,6 @@ constexpr int kCtrSlots = 64;       // striped copies of the work counters
 constexpr int kChunkMax = RT_CHUNK_MAX; // slots a wave takes from the trace queue per atomic...
 constexpr int kChunkMin = 64;        // ...shrunk so that every wave gets ~4 chunks when few rays live
 constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are idle
- // leaf triangles whose loads are issued together
 constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffer set each)
 constexpr int kTraceOccPct = RT_TRACE_OCC; // % of the resident trace workgroups the persistent grid uses
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
@@ -84,6 +83,14 @@ struct DevScene {
     V3 cam, tl, sr, su, min_coord, inv_dim;
     float inv_w, inv_h;
 };
+
+#ifdef RT_PROFILE
+// Wave-level traversal profile (debug builds only): see tools/variants.sh + RT_PROFILE=1.
+__device__ unsigned long long g_prof[8];
+#define PROF(i, v) (prof[i] += (v))
+#else
+#define PROF(i, v) ((void)0)
+#endif
 
 struct Counters {                     // device-side work counters (u64, one atomic per wave)
     unsigned long long live, pn, iv, tt, st, hits, misses, hits_sphere;
@@ -122,6 +129,34 @@ __device__ __forceinline__ V3 primary_dir(const DevScene &S, int i, const PassAr
 }
 
 // ---------------------------------------------------------------- traversal
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Both children's slab tests (ray_aabb_intersection, scene.cu:109-132) on the interleaved node
+// record {lx0 lx1 ly0 ly1} {lz0 lz1 hx0 hx1} {hy0 hy1 hz0 hz1}: the plane distances of the two
+// boxes share packed-fp32 ops.  The reference folds the three axes in sequence,
+//   tmin = fminf(fmaxf(t1, tmin), fmaxf(t2, tmin)),  tmax = fmaxf(fminf(t1, tmax), fminf(t2, tmax)),
+// which for NaN-free t1/t2 is exactly tmin = max(min_x, min_y, min_z, 0) and
+// tmax = min(max_x, max_y, max_z, closest) (min/max do not round; zero signs never reach a
+// comparison outcome).  t is NaN only for 0 * inf, so the caller uses this form only when all of
+// 1/d is finite and otherwise the literal per-axis fold (slab()).
+__device__ __forceinline__ void slab_pair(float4 a, float4 b, float4 c, V3 o, float ix, float iy, float iz,
+                                          float closest, bool &h0, bool &h1, float &t0, float &t1) {
+    const f2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const f2 vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz};
+    const f2 lx = {a.x, a.y}, ly = {a.z, a.w}, lz = {b.x, b.y};
+    const f2 hx = {b.z, b.w}, hy = {c.x, c.y}, hz = {c.z, c.w};
+    const f2 x1 = (lx - ox) * vx, x2 = (hx - ox) * vx;
+    const f2 y1 = (ly - oy) * vy, y2 = (hy - oy) * vy;
+    const f2 z1 = (lz - oz) * vz, z2 = (hz - oz) * vz;
+    const float n0 = fmaxf(fmaxf(fminf(x1.x, x2.x), fminf(y1.x, y2.x)), fmaxf(fminf(z1.x, z2.x), 0.0f));
+    const float f0 = fminf(fminf(fmaxf(x1.x, x2.x), fmaxf(y1.x, y2.x)), fminf(fmaxf(z1.x, z2.x), closest));
+    const float n1 = fmaxf(fmaxf(fminf(x1.y, x2.y), fminf(y1.y, y2.y)), fmaxf(fminf(z1.y, z2.y), 0.0f));
+    const float f1 = fminf(fminf(fmaxf(x1.y, x2.y), fmaxf(y1.y, y2.y)), fminf(fmaxf(z1.y, z2.y), closest));
+    t0 = n0; t1 = n1;
+    h0 = n0 <= f0;
+    h1 = n1 <= f1;
+}
+
 // Triangle range [ti, te) of a leaf ref (small leaves inline, big ones through big_leaves).
 __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int &ti, int &te) {
     if (ref & kBigLeaf) {
@@ -165,14 +200,19 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
     int slot = -1;                      // < 0: lane has no ray
     V3 o{0, 0, 0}, d{0, 0, 0};
     float ix = 0, iy = 0, iz = 0, closest = 0;
+    bool finite_inv = true;
     int index = -1, sp = 0;
     uint32_t ref = 0;
     int ti = 0, te = 0;                 // the lane is in a leaf while ti < te
     unsigned pn = 0, iv = 0, tt = 0, nlive = 0;
+#ifdef RT_PROFILE
+    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     while (true) {
         // ---- refill idle lanes (wave-uniform control flow)
         unsigned long long idle = __ballot(slot < 0);
         if (!exhausted && __popcll(idle) >= kRefill) {
+            PROF(6, 1);
             bool fresh = false;
             while (idle && !exhausted) {
                 if (q_next >= q_end) {
@@ -213,6 +253,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
                         d = v3(r0.w, r1.x, r1.y);
                     }
                     ix = 1 / d.x; iy = 1 / d.y; iz = 1 / d.z;
+                    finite_inv = __builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz);
                     closest = 1e30f;
                     index = -1;
                     for (int i = 0; i < S.sphere_count; i++) {
@@ -236,19 +277,33 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
         }
         if (!__ballot(slot >= 0)) {
             if (exhausted) break;
+            PROF(7, 1);
             continue;
         }
+#ifdef RT_PROFILE
+        {
+            const unsigned long long act = __ballot(slot >= 0), lf = __ballot(slot >= 0 && ti < te);
+            PROF(0, 1); PROF(1, __popcll(act)); PROF(2, __popcll(lf));
+            PROF(3, lf != 0); PROF(4, (act & ~lf) != 0);
+        }
+#endif
         if (slot < 0) continue;
         // ---- one step: a single triangle test of the current leaf, or one internal node
         // (both children's slabs).  One triangle per step keeps the leaf branch as short as the
         // internal one, so lanes at leaves and lanes at internal nodes share a step at ~50 %
         // SIMD efficiency instead of the whole wave running a leaf's worth of triangle tests.
         // The node/triangle visit order per lane is the reference's (scene.cu:145-238).
+        // Both kinds of step read their record through the same loads (a triangle's p1 e1 e2, or a
+        // node's interleaved child bounds and child refs), issued before the branch, so a step
+        // costs one memory round trip whatever mix of leaf and internal lanes the wave holds.
         bool need = false;              // the lane needs the next node from its stack
-        if (ti < te) {
-            const float4 *tp = S.tris + (size_t)ti * 3;
-            const float4 q0 = tp[0], q1 = tp[1];
-            const float q2 = tp[2].x;
+        const bool in_leaf = ti < te;
+        const float4 *rec = in_leaf ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4;
+        const float4 a = rec[0], b = rec[1], c = rec[2];
+        const uint2 kids = *reinterpret_cast<const uint2 *>(rec + 3);   // node lanes only use it
+        if (in_leaf) {
+            const float4 q0 = a, q1 = b;
+            const float q2 = c.x;
             if (COUNT) tt++;
             float t;
             if (ray_triangle(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t)) {
@@ -258,12 +313,14 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
             need = ++ti == te;
         } else {
             if (COUNT) iv++;
-            const float4 *nd = S.nodes + (size_t)ref * 4;
-            const float4 a = nd[0], b = nd[1], c = nd[2];
-            const uint4 kids = *reinterpret_cast<const uint4 *>(nd + 3);
             float t0, t1;
-            const bool h0 = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, ix, iy, iz, closest, t0);
-            const bool h1 = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, ix, iy, iz, closest, t1);
+            bool h0, h1;
+            if (__builtin_expect(finite_inv, 1)) {
+                slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
+            } else {            // some 1/d component is infinite: 0 * inf may give NaN
+                h0 = slab(a.x, a.z, b.x, b.z, c.x, c.z, o, ix, iy, iz, closest, t0);
+                h1 = slab(a.y, a.w, b.y, b.w, c.y, c.w, o, ix, iy, iz, closest, t1);
+            }
             bool descend = false;
             if (h0 && h1) {
                 // The reference pushes near then far (scene.cu:204-225): the far child is next.
@@ -295,6 +352,9 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
                 }
             }
         }
+#ifdef RT_PROFILE
+        if (__ballot(need)) PROF(5, 1);
+#endif
         while (need) {                  // pop to the next entry nearer than closest
             if (sp == 0) {
                 hits[slot] = make_float2(closest, __int_as_float(index));
@@ -334,6 +394,10 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
         }
     }
     if (lane_id() == 0 && nl) atomicAdd(&cs->live, nl);
+#ifdef RT_PROFILE
+    if (lane_id() == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(&g_prof[i], prof[i]);
+#endif
 }
 
 // Shading for the live slots (scene.cu:376-485): environment lookup on a miss, otherwise
@@ -625,10 +689,12 @@ struct DevBuf {
         HIPCHK(hipMalloc(reinterpret_cast<void **>(&p), count * sizeof(T)));
         return RT_OK;
     }
-    int upload(const void *src, size_t count, hipStream_t s) {
-        int rc = alloc(count);
+    // `pad` zeroed elements after the copied ones (readable slack for over-wide loads)
+    int upload(const void *src, size_t count, hipStream_t s, size_t pad = 0) {
+        int rc = alloc(count + pad);
         if (rc) return rc;
         if (count) HIPCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+        if (pad) HIPCHK(hipMemsetAsync(p + count, 0, pad * sizeof(T), s));
         return RT_OK;
     }
 };
@@ -730,9 +796,10 @@ struct rt_renderer {
             if (nd.child1 < 0 || nd.child2 >= nn) return rtamd::fail(RT_E_INVALID, "BVH child index out of range");
             const rt_bvh_node &l = sc->bvh[nd.child1], &r = sc->bvh[nd.child2];
             float4 *q = &rec_h[(size_t)rec[i] * 4];
-            q[0] = make_float4(l.min_bound.x, l.min_bound.y, l.min_bound.z, l.max_bound.x);
-            q[1] = make_float4(l.max_bound.y, l.max_bound.z, r.min_bound.x, r.min_bound.y);
-            q[2] = make_float4(r.min_bound.z, r.max_bound.x, r.max_bound.y, r.max_bound.z);
+            // the two children's bounds interleaved per plane, so one packed-fp32 op handles both
+            q[0] = make_float4(l.min_bound.x, r.min_bound.x, l.min_bound.y, r.min_bound.y);
+            q[1] = make_float4(l.min_bound.z, r.min_bound.z, l.max_bound.x, r.max_bound.x);
+            q[2] = make_float4(l.max_bound.y, r.max_bound.y, l.max_bound.z, r.max_bound.z);
             const uint32_t a = ref_of(nd.child1), b = ref_of(nd.child2);
             std::memcpy(&q[3].x, &a, 4);
             std::memcpy(&q[3].y, &b, 4);
@@ -741,7 +808,8 @@ struct rt_renderer {
         ds.root_ref = nn > 0 ? ref_of(0) : (kLeaf | 0u);
         if (big_h.empty()) big_h.push_back(make_int2(0, 0));
         if ((rc = spheres.upload(sc->spheres, sc->sphere_count, s0))) return rc;
-        if ((rc = tris.upload(sc->triangles, (size_t)sc->triangle_count * 3, s0))) return rc;
+        // one float4 of slack: traversal reads 64 B at a triangle record (48 B) like at a node
+        if ((rc = tris.upload(sc->triangles, (size_t)sc->triangle_count * 3, s0, 1))) return rc;
         if ((rc = mats.upload(sc->materials, (size_t)sc->material_count * 3, s0))) return rc;
         if ((rc = mat_idx.upload(sc->material_indices, (size_t)sc->sphere_count + sc->triangle_count, s0))) return rc;
         if ((rc = nodes.upload(rec_h.data(), rec_h.size(), s0))) return rc;
@@ -912,6 +980,18 @@ struct rt_renderer {
         }
         HIPCHK(hipEventRecord(t_end, s0));
         HIPCHK(hipStreamSynchronize(s0));
+#ifdef RT_PROFILE
+        {
+            unsigned long long pr[8];
+            HIPCHK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof(pr)));
+            const double it = (double)pr[0];
+            std::fprintf(stderr, "RT_PROFILE wave_iters %llu active/iter %.2f leaf/iter %.2f iters_with_leaf %.3f "
+                         "iters_with_inner %.3f iters_with_pop %.3f refills/iter %.3f idle_iters %llu\n",
+                         pr[0], pr[1] / it, pr[2] / it, pr[3] / it, pr[4] / it, pr[5] / it, pr[6] / it, pr[7]);
+            std::memset(pr, 0, sizeof(pr));
+            HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));
+        }
+#endif
         if (st) {
             std::memset(st, 0, sizeof(*st));
             std::vector<Counters> slots(kCtrSlots);
