@@ -25,10 +25,11 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-# The renderer keeps 4 passes in flight on 4 streams; with torch/RCCL streams in the same process
-# HIP's default of 4 hardware queues would make them share queues.  Set before HIP initialises.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# The renderer keeps up to 12 passes in flight on their own streams; with torch/RCCL streams in the
+# same process HIP's default of 4 hardware queues would make them share queues.  Set before HIP
+# initialises.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 sys.path.insert(0, os.path.join(REPO, "cuda-raytracer_amd"))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 
@@ -100,8 +101,9 @@ def cpu_baseline(cfg, args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="passes per GPU to time (default: one full frame, ceil(passes/N) per GPU)")
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--scene", default="teapot", choices=sorted(CONFIGS))
     ap.add_argument("--no-sort", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=8)
@@ -143,49 +145,54 @@ def main():
     stats_acc = {}
 
     def accumulate_stats(st):
-        for k in ("live_segments", "generated_rays"):
-            stats_acc[k] = stats_acc.get(k, 0) + st[k]
-        for k in ("process_ms", "sort_ms", "kernel_ms"):
-            stats_acc[k] = stats_acc.get(k, 0.0) + st[k]
+        for k, v in st.items():
+            if isinstance(v, (int, float)):
+                stats_acc[k] = stats_acc.get(k, 0) + v
 
     def render_passes(passes, out):
-        # passes are r, r+N, r+2N, ...: one renderer call keeps two of them in flight
+        # passes are r, r+N, r+2N, ...: one renderer call keeps several of them in flight
         stride = passes[1] - passes[0] if len(passes) > 1 else 1
         accumulate_stats(ren.run(pass_begin=passes[0], count=len(passes), stride=stride,
                                  d_pass_sums=out.data_ptr()))
 
+    R = -(-P // world)                  # rounds (one pass per GPU each) per frame
+    full_frame = args.steps is None
+    steps = R if full_frame else args.steps
     if use_dist:
         import rtamd_dist
-        frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, torch.device("cuda", local), render_passes)
+        frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, torch.device("cuda", local), render_passes,
+                                            max_rounds_per_call=32)
 
     def barrier_sync():
         if use_dist:
             dist.barrier()
             torch.cuda.synchronize()
 
-    def run_steps(first, k, stats):
-        """Steps first .. first+k-1 (one pass per GPU each)."""
+    def run_steps(k, stats):
+        """k steps from the first pass of the frame, wrapping at its end; one pass per GPU per
+        step (rank r renders passes r, r+N, ...).  Returns the passes this rank rendered."""
         stats_acc.clear()
-        if k <= 0:
-            return
-        if use_dist:
-            # this rank's passes of those rounds, then per round an RCCL gather of the pass
-            # framebuffers to rank 0, which adds them in pass order (rtamd_dist.PassShardedFrame)
-            frame.run_rounds(first, k)
-        else:
-            accumulate_stats(ren.run(pass_begin=first % P, count=min(k, P - first % P), stride=1))
+        done = mine = 0
+        while done < k:
+            m = min(k - done, R)
+            if use_dist:
+                # this rank's passes of those rounds, then per round an RCCL gather of the pass
+                # framebuffers to rank 0, which adds them in pass order (rtamd_dist.PassShardedFrame)
+                mine += frame.run_rounds(0, m)
+            else:
+                accumulate_stats(ren.run(pass_begin=0, count=m, stride=1))
+                mine += m
+            done += m
         for key, v in stats_acc.items():
             stats[key] = stats.get(key, 0) + v
-
-    def pass_of(step):
-        return (rank + world * step) % P
+        return mine
 
     warm = {}
-    run_steps(0, args.warmup, warm)
+    run_steps(args.warmup, warm)
     barrier_sync()
     timed = {}
     t0 = time.perf_counter()
-    run_steps(args.warmup, args.steps, timed)
+    my_passes = run_steps(steps, timed)
     barrier_sync()
     elapsed = time.perf_counter() - t0
 
@@ -201,30 +208,31 @@ def main():
 
     # Byte model: recount the timed passes with the counting kernel variant (untimed).
     counted = None
-    if not args.no_counters and args.steps > 0:
+    if not args.no_counters and steps > 0:
         ren.set_counters(True)
         counted = {}
-        first = pass_of(args.warmup)
-        st = ren.run(pass_begin=first, count=max(1, min(args.steps, (P - 1 - first) // world + 1)), stride=world)
-        for k, v in st.items():
-            if isinstance(v, int):
-                counted[k] = counted.get(k, 0) + v
+        run_steps(steps, counted)
+        counted = {k: int(v) for k, v in counted.items() if isinstance(v, int)}
         counted["dead_slot_bytes"] = 0 if sort else counted["dead_slots"]
         ren.set_counters(False)
+    bytes_total = segment_bytes(counted, scene.view.sphere_count) if counted else 0.0
+    launches = my_passes * bounces
+    if use_dist:
+        t = torch.tensor([bytes_total, launches], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        bytes_total, launches = float(t[0].item()), int(t[1].item())
 
     if rank == 0:
         workload = "%s %dx%d %dspp %d bounces sort=%s" % (scene_file, W, H, spp, bounces, "on" if sort else "off")
-        launches = args.steps * bounces
-        ms_launch = proc_ms / launches if launches else 0.0
+        ms_launch = proc_ms / (my_passes * bounces) if my_passes else 0.0
         roof = None
         if counted:
-            bytes_total = segment_bytes(counted, scene.view.sphere_count)
             bytes_launch = bytes_total / launches
-            # Up to 4 passes are in flight, so process launches of different passes overlap and a
+            # Up to 12 passes are in flight, so process launches of different passes overlap and a
             # launch's own duration overstates its share of the GPU: `achieved` is the process
             # kernels' algorithmic bytes over the wall time of the timed steps (conservative: the
-            # wall also covers generate/reorder/accumulate); the per-launch figure is reported too.
-            achieved = bytes_total * world / elapsed / 1e9 if elapsed > 0 else 0.0
+            # wall also covers reorder/accumulate); the per-launch figure is reported too.
+            achieved = bytes_total / elapsed / 1e9 if elapsed > 0 else 0.0
             per_launch = bytes_launch / (ms_launch / 1e3) / 1e9 if ms_launch > 0 else 0.0
             traffic = load_pmc(workload)
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -236,30 +244,37 @@ def main():
                              "dead slots: 0 B with sort (never visited), 1 B without; counts from the device "
                              "counters of the same passes; achieved = bytes of all process launches / timed wall"}
         value = live / elapsed / 1e6 if elapsed > 0 else 0.0
-        nominal = world * args.steps * 20 * W * H * bounces / elapsed / 1e6 if elapsed > 0 else 0.0
-        ms_step = elapsed / args.steps * 1e3 if args.steps else 0.0
+        gen = timed.get("generated_rays", 0)
+        if use_dist:
+            t = torch.tensor([gen], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t)
+            gen = int(t.item())
+        nominal = gen * bounces / elapsed / 1e6 if elapsed > 0 else 0.0
+        ms_step = elapsed / steps * 1e3 if steps else 0.0
         out = {
             "metric": "Mrays/s (live ray segments/s, %s)" % args.scene,
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if full_frame else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: reference scene + assets, procedural stand-in env map (assets missing upstream)",
             "config": {
                 "workload": workload,
                 "step": "one 20-spp pass (%d rays x %d bounces) per GPU; pass-sharded over GPUs" % (20 * W * H, bounces),
+                "timed": ("one full frame (%d passes)" % P) if full_frame else ("%d passes per GPU" % steps),
                 "parallelism": "pass-shard x%d + RCCL gather" % world if world > 1 else "single GPU",
                 "nominal_mrays_per_s": round(nominal, 2),
-                "render_wall_ms_projected": round(ms_step * -(-P // world), 1),
+                "render_wall_ms": round(elapsed * 1e3, 1) if full_frame else None,
+                "render_wall_ms_projected": round(ms_step * R, 1),
                 "passes_per_frame": P,
-                "process_ms_per_step": round(proc_ms / max(args.steps, 1), 3),
-                "sort_ms_per_step": round(timed.get("sort_ms", 0.0) / max(args.steps, 1), 3),
+                "process_ms_per_step": round(proc_ms / max(my_passes, 1), 3),
+                "sort_ms_per_step": round(timed.get("sort_ms", 0.0) / max(my_passes, 1), 3),
                 "scene_load_s": round(load_s, 3),
                 "bvh_ms": round(scene.bvh_ms, 1),
             },

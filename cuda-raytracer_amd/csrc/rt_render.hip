@@ -45,7 +45,7 @@ namespace {
 #define RT_CHUNK_MAX 128
 #endif
 #ifndef RT_INFLIGHT
-#define RT_INFLIGHT 4
+#define RT_INFLIGHT 12
 #endif
 #ifndef RT_TRACE_OCC
 #define RT_TRACE_OCC 75
@@ -744,6 +744,7 @@ struct rt_renderer {
     DevBuf<Counters> ctr;
     PassCtx ctx[kInflight];
     int trace_blocks = 0;             // persistent trace_kernel grid
+    int nctx = 1;                     // pass contexts allocated (passes in flight)
     int cus = 0;
     hipEvent_t t_begin = nullptr, t_end = nullptr;
 
@@ -826,7 +827,15 @@ struct rt_renderer {
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<true, false, false>, kBlock, 0));
         trace_blocks = std::max(1, cus * std::max(1, per_cu) * kTraceOccPct / 100);
         const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
-        const int inflight = std::min(kInflight, std::max(1, pass_count()));
+        // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
+        // than half of the free device memory holds (1080p: ~2.9 GB per context).
+        const size_t ctx_bytes = (size_t)max_rays * (32 + 16 + 8 + 8 + (sort ? 10 : 0)) +
+                                 (size_t)trace_blocks * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
+        size_t mem_free = 0, mem_total = 0;
+        HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
+        nctx = (int)std::min<size_t>({(size_t)kInflight, (size_t)std::max(1, pass_count()),
+                                      std::max<size_t>(1, mem_free / 2 / ctx_bytes)});
+        const int inflight = nctx;
         for (int k = 0; k < inflight; k++) {
             PassCtx &c = ctx[k];
             if ((rc = c.geo.alloc((size_t)max_rays * 2))) return rc;
@@ -942,7 +951,7 @@ struct rt_renderer {
         return RT_OK;
     }
 
-    // Passes pass_begin + k*stride, k < count, kInflight at a time on separate streams; the
+    // Passes pass_begin + k*stride, k < count, nctx at a time on separate streams; the
     // framebuffer adds stay in pass order through cross-stream events.
     int run(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st) {
         const auto w0 = std::chrono::high_resolution_clock::now();
@@ -952,7 +961,7 @@ struct rt_renderer {
         if (count < 0) count = pass_begin < P ? (P - pass_begin + stride - 1) / stride : 0;
         if (pass_begin < 0 || (count > 0 && pass_begin + (int64_t)(count - 1) * stride >= P))
             return rtamd::fail(RT_E_INVALID, "pass range outside the render");
-        const int inflight = std::min(kInflight, std::max(1, P));
+        const int inflight = std::min(nctx, std::max(1, P));
         hipStream_t s0 = stream();
         HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, s0));
         HIPCHK(hipEventRecord(t_begin, s0));

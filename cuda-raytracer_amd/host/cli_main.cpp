@@ -79,8 +79,9 @@ int render_multi(const rt_scene *s, int sort, int ndev, std::vector<float> &fb, 
 }  // namespace
 
 int main(int argc, char **argv) {
-    // 4 passes in flight per device on 4 streams: give HIP enough hardware queues (read at init).
-    if (const char *q = std::getenv("GPU_MAX_HW_QUEUES"); !q || std::atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+    // Up to 12 passes in flight per device on their own streams: give HIP enough hardware queues
+    // (read when HIP initialises).
+    if (const char *q = std::getenv("GPU_MAX_HW_QUEUES"); !q || std::atoi(q) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
     if (argc < 2) {
         std::printf("Usage: %s <scene>\n", argv[0]);
         return 1;

@@ -26,7 +26,7 @@ class PassShardedFrame:
 
     render_passes(passes, out) must write pass passes[j]'s per-pixel sum (W*H*3 float32) into
     out[j], a 2-D tensor on `device`; handing several passes to one call lets the renderer keep
-    two passes in flight.  Rank 0 owns the accumulated framebuffer `fb`.
+    several passes in flight.  Rank 0 owns the accumulated framebuffer `fb`.
     """
 
     def __init__(self, dist, torch, pixels3: int, passes: int, device, render_passes: Callable,
