@@ -606,21 +606,36 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
 // ---------------------------------------------------------------- accumulate
 // Ordered per-pixel sum of the pass's samples (the caller then adds it: fb += sum, in pass order) (raytracing.cu:96-107 without
 // the unordered atomics; the CPU path's order, raytracing.cu:114-120).
+// A block stages the samples of kAccPixels consecutive pixels (contiguous in tc, pixel-major)
+// through LDS with coalesced loads, then one lane per pixel sums them in sample order.
+constexpr int kAccPixels = 64;
 __global__ __launch_bounds__(kBlock) void accumulate_kernel(const float4 *__restrict__ tc, int rtc, int pixels,
                                                             float *__restrict__ sums) {
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= pixels) return;
-    float sx = 0, sy = 0, sz = 0;
-    const float4 *r = tc + (size_t)p * rtc;
-    for (int s = 0; s < rtc; s++) {
-        const float4 c = r[s];
-        sx = sx + c.y;
-        sy = sy + c.z;
-        sz = sz + c.w;
+    __shared__ float col[kAccPixels * 20 * 3];
+    const int p0 = blockIdx.x * kAccPixels;
+    const int np = min(kAccPixels, pixels - p0);
+    const int n = np * rtc;
+    const float4 *src = tc + (size_t)p0 * rtc;
+    for (int e = threadIdx.x; e < n; e += kBlock) {
+        const float4 c = src[e];
+        col[e * 3] = c.y;
+        col[e * 3 + 1] = c.z;
+        col[e * 3 + 2] = c.w;
     }
-    sums[(size_t)p * 3] = sx;
-    sums[(size_t)p * 3 + 1] = sy;
-    sums[(size_t)p * 3 + 2] = sz;
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t >= np) return;
+    float sx = 0, sy = 0, sz = 0;
+    const float *r = col + t * rtc * 3;
+    for (int s = 0; s < rtc; s++) {
+        sx = sx + r[s * 3];
+        sy = sy + r[s * 3 + 1];
+        sz = sz + r[s * 3 + 2];
+    }
+    const size_t p = (size_t)(p0 + t);
+    sums[p * 3] = sx;
+    sums[p * 3 + 1] = sy;
+    sums[p * 3 + 2] = sz;
 }
 
 // ---------------------------------------------------------------- bloom (raytracing.cu:21-74)
@@ -944,8 +959,8 @@ struct rt_renderer {
             // rays were generated with collected = 0 and never processed (raytracing.cu:232)
             HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
         } else {
-            hipLaunchKernelGGL(accumulate_kernel, dim3(blocks_for(pixels)), dim3(kBlock), 0, st, c.tc.p, rtc,
-                               (int)pixels, sums);
+            hipLaunchKernelGGL(accumulate_kernel, dim3((unsigned)((pixels + kAccPixels - 1) / kAccPixels)), dim3(kBlock),
+                               0, st, c.tc.p, rtc, (int)pixels, sums);
         }
         HIPCHK(hipGetLastError());
         return RT_OK;
