@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr) {
-    __shared__ uint2 stack[kStackLds * kBlock];
+    __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
     uint2 *col = stack + threadIdx.x;
     // Overflow tail of the stack (entries >= kStackLds, rare) in a global per-lane buffer,
     // [entry][lane] for coalescing; stored as two 32-bit arrays so the compiler cannot fuse the
@@ -315,34 +315,34 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
             if (COUNT) iv++;
             float t0, t1;
             bool h0, h1;
-            if (__builtin_expect(finite_inv, 1)) {
-                slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
-            } else {            // some 1/d component is infinite: 0 * inf may give NaN
-                h0 = slab(a.x, a.z, b.x, b.z, c.x, c.z, o, ix, iy, iz, closest, t0);
-                h1 = slab(a.y, a.w, b.y, b.w, c.y, c.w, o, ix, iy, iz, closest, t1);
+            slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
+            if (__builtin_expect(__ballot(!finite_inv) != 0, 0)) {
+                // some lane's 1/d has an infinite component (0 * inf may give NaN): the literal
+                // per-axis fold for those lanes
+                float u0, u1;
+                const bool g0 = slab(a.x, a.z, b.x, b.z, c.x, c.z, o, ix, iy, iz, closest, u0);
+                const bool g1 = slab(a.y, a.w, b.y, b.w, c.y, c.w, o, ix, iy, iz, closest, u1);
+                if (!finite_inv) { h0 = g0; h1 = g1; t0 = u0; t1 = u1; }
             }
-            bool descend = false;
-            if (h0 && h1) {
-                // The reference pushes near then far (scene.cu:204-225): the far child is next.
-                uint2 below;
-                float ttop;
-                if (t0 < t1) { below = make_uint2(kids.x, __float_as_uint(t0)); ref = kids.y; ttop = t1; }
-                else { below = make_uint2(kids.y, __float_as_uint(t1)); ref = kids.x; ttop = t0; }
-                if (__builtin_expect(sp < kStackLds, 1)) {
-                    col[sp * kBlock] = below;
-                } else {
-                    ovf_ref[(sp - kStackLds) * lanes] = below.x;
-                    ovf_dist[(sp - kStackLds) * lanes] = __uint_as_float(below.y);
-                }
-                sp++;
-                descend = !(ttop >= closest);
-            } else if (h0) {
-                ref = kids.x;
-                descend = !(t0 >= closest);
-            } else if (h1) {
-                ref = kids.y;
-                descend = !(t1 >= closest);
+            // The reference pushes the hit children near then far (scene.cu:204-225) and pops the
+            // top: with both hit the far child is next and the near one stays on the stack; with
+            // one hit that one is next.  Next is entered unless its entry distance >= closest.
+            const bool both = h0 & h1, any = h0 | h1;
+            const bool x_near = t0 < t1;
+            const uint32_t near_ref = x_near ? kids.x : kids.y, far_ref = x_near ? kids.y : kids.x;
+            const float near_t = x_near ? t0 : t1, far_t = x_near ? t1 : t0;
+            const uint32_t next_ref = both ? far_ref : (h0 ? kids.x : kids.y);
+            const float next_t = both ? far_t : (h0 ? t0 : t1);
+            // the near child is written either way (above the top when not pushed; entry
+            // kStackLds is a scratch slot), so the push needs no branch
+            col[min(sp, kStackLds) * kBlock] = make_uint2(near_ref, __float_as_uint(near_t));
+            if (__builtin_expect(both & (sp >= kStackLds), 0)) {
+                ovf_ref[(sp - kStackLds) * lanes] = near_ref;
+                ovf_dist[(sp - kStackLds) * lanes] = near_t;
             }
+            sp += both ? 1 : 0;
+            ref = any ? next_ref : ref;
+            const bool descend = any & !(next_t >= closest);
             need = !descend;
             if (descend) {
                 if (COUNT) pn++;
