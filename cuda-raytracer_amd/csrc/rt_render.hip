@@ -771,7 +771,8 @@ struct rt_renderer {
     hipStream_t stream() const { return ctx[0].stream; }
     int pass_count() const { return (spp + 19) / 20; }
 
-    int init(const rt_scene *sc, const rt_opts *o) {
+    // passes = false: scene only (rt_trace_rays), no pass contexts
+    int init(const rt_scene *sc, const rt_opts *o, bool passes = true) {
         device = o->device;
         sort = o->sort != 0;
         counters = o->collect_counters != 0;
@@ -848,8 +849,8 @@ struct rt_renderer {
                                  (size_t)trace_blocks * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
         size_t mem_free = 0, mem_total = 0;
         HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
-        nctx = (int)std::min<size_t>({(size_t)kInflight, (size_t)std::max(1, pass_count()),
-                                      std::max<size_t>(1, mem_free / 2 / ctx_bytes)});
+        nctx = !passes ? 0 : (int)std::min<size_t>({(size_t)kInflight, (size_t)std::max(1, pass_count()),
+                                                    std::max<size_t>(1, mem_free / 2 / ctx_bytes)});
         const int inflight = nctx;
         for (int k = 0; k < inflight; k++) {
             PassCtx &c = ctx[k];
@@ -963,6 +964,61 @@ struct rt_renderer {
                                0, st, c.tc.p, rtc, (int)pixels, sums);
         }
         HIPCHK(hipGetLastError());
+        return RT_OK;
+    }
+
+    // Closest hit of n caller rays (o.xyz, d.xyz; d unit length like every ray of the render):
+    // the sphere loop and BVH traversal of one bounce (scene.cu:338-372, :134-241) through the
+    // same trace_kernel as the render, without shading.
+    int trace_rays(const float *rays, int n, float *t_out, int32_t *index_out, rt_stats *st) {
+        HIPCHK(hipSetDevice(device));
+        if (n <= 0) return RT_OK;
+        hipStream_t s0 = stream();
+        std::vector<float4> g((size_t)n * 2);
+        for (int i = 0; i < n; i++) {
+            const float *r = rays + (size_t)i * 6;
+            g[(size_t)i * 2] = make_float4(r[0], r[1], r[2], r[3]);
+            g[(size_t)i * 2 + 1] = make_float4(r[4], r[5], 1.0f, 1.0f);
+        }
+        DevBuf<float4> geo;
+        DevBuf<uint8_t> bkt;
+        DevBuf<uint32_t> live, queue, overflow;
+        DevBuf<float2> hits;
+        int rc;
+        if ((rc = geo.upload(g.data(), g.size(), s0))) return rc;
+        if ((rc = bkt.alloc((size_t)n)) || (rc = live.alloc(1)) || (rc = queue.alloc((size_t)kQueues * kQueueStride)) ||
+            (rc = hits.alloc((size_t)n)) || (rc = overflow.alloc((size_t)trace_blocks * kBlock * 2 * (kStackMax - kStackLds))))
+            return rc;
+        HIPCHK(hipMemsetAsync(bkt.p, 0, (size_t)n, s0));
+        HIPCHK(hipMemsetAsync(queue.p, 0, queue.n * sizeof(uint32_t), s0));
+        const uint32_t nn = (uint32_t)n;
+        HIPCHK(hipMemcpyAsync(live.p, &nn, sizeof(nn), hipMemcpyHostToDevice, s0));
+        HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, s0));
+        const PassArgs pa{1, 0u};
+        const int tgrid = std::min(blocks_for(n), trace_blocks);
+        if (counters)
+            hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
+                               nullptr, bkt.p, live.p, queue.p, hits.p, overflow.p, ctr.p);
+        else
+            hipLaunchKernelGGL((trace_kernel<false, false, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
+                               nullptr, bkt.p, live.p, queue.p, hits.p, overflow.p, ctr.p);
+        HIPCHK(hipGetLastError());
+        std::vector<float2> h((size_t)n);
+        HIPCHK(hipMemcpyAsync(h.data(), hits.p, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, s0));
+        HIPCHK(hipStreamSynchronize(s0));
+        for (int i = 0; i < n; i++) {
+            if (t_out) t_out[i] = h[i].x;
+            if (index_out) std::memcpy(&index_out[i], &h[i].y, 4);
+        }
+        if (st) {
+            std::memset(st, 0, sizeof(*st));
+            std::vector<Counters> slots(kCtrSlots);
+            HIPCHK(hipMemcpy(slots.data(), ctr.p, sizeof(Counters) * kCtrSlots, hipMemcpyDeviceToHost));
+            for (const Counters &x : slots) {
+                st->live_segments += x.live; st->nodes_popped += x.pn; st->internal_visits += x.iv;
+                st->triangle_tests += x.tt; st->sphere_tests += x.st;
+            }
+        }
         return RT_OK;
     }
 
@@ -1191,6 +1247,21 @@ int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stat
     delete r;
     if (!rc && stats)
         stats->render_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
+    return rc;
+}
+
+int rt_trace_rays(const rt_scene *scene, const rt_opts *opts, const float *rays, int32_t n, float *t_out,
+                  int32_t *index_out, rt_stats *stats) {
+    if (n < 0 || (n > 0 && !rays)) return rtamd::fail(RT_E_INVALID, "rt_trace_rays: bad argument");
+    int rc = check_scene(scene);
+    if (rc) return rc;
+    rt_opts o;
+    if (opts) o = *opts; else rt_default_opts(&o);
+    if (rt_device_count() <= o.device || o.device < 0) return rtamd::fail(RT_E_NODEVICE, "no such HIP device");
+    auto *r = new rt_renderer();
+    rc = r->init(scene, &o, false);
+    if (!rc) rc = r->trace_rays(rays, n, t_out, index_out, stats);
+    delete r;
     return rc;
 }
 

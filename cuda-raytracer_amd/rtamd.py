@@ -106,6 +106,7 @@ def lib():
         L.rt_renderer_clear.argtypes = [P]
         L.rt_renderer_set_counters.argtypes = [P, I32]
         L.rt_renderer_destroy.argtypes = [P]
+        L.rt_trace_rays.argtypes = [P, P, P, I32, P, P, P]
         L.rt_bloom.argtypes = [P, I32, I32, C.c_float, I32, I32]
         L.rt_bloom_device.argtypes = [P, I32, I32, C.c_float, I32, I32]
         L.rt_tonemap.argtypes = [P, I32, I32, C.c_float, I32, P]
@@ -219,6 +220,18 @@ def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=
     o = default_opts(sort, device, pass_begin, pass_count, pass_stride, counters)
     _check(lib().rt_render(scene.ptr, C.byref(o), _ptr(fb), C.byref(st)))
     return fb, st.as_dict()
+
+
+def trace_rays(scene, rays, device=0, counters=False):
+    """rt_trace_rays: closest hit of rays (n, 6) float32 {o.xyz, d.xyz}.  Returns (t, index, stats)."""
+    rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+    n = rays.shape[0]
+    t = np.zeros(n, np.float32)
+    idx = np.zeros(n, np.int32)
+    st = RtStats()
+    o = default_opts(True, device, counters=counters)
+    _check(lib().rt_trace_rays(scene.ptr, C.byref(o), _ptr(rays), n, _ptr(t), _ptr(idx), C.byref(st)))
+    return t, idx, st.as_dict()
 
 
 class Renderer:

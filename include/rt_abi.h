@@ -128,7 +128,7 @@ int rt_device_count(void);
 int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stats *stats);
 
 /* Persistent renderer: scene resident in HBM, ray buffers sized for 20 rays/pixel per pass,
- * up to 4 passes in flight on separate streams (each with its own buffer set) so one pass's
+ * up to 12 passes in flight on separate streams (each with its own buffer set) so one pass's
  * latency-bound last bounces overlap another's throughput-bound first bounces.  The framebuffer
  * adds stay in pass order.  Used by rt_render, the benchmark and the multi-GPU drivers. */
 typedef struct rt_renderer rt_renderer;
@@ -146,6 +146,15 @@ int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out);   /* device fb 
 int rt_renderer_clear(rt_renderer *r);                               /* zero the device fb    */
 int rt_renderer_set_counters(rt_renderer *r, int32_t enable);
 void rt_renderer_destroy(rt_renderer *r);
+
+/* Closest hit of n caller rays: rays = n x {o.x o.y o.z d.x d.y d.z} (d unit length, as every
+ * ray the render traces).  The sphere loop (scene.cu:338-372) then bvh_closest_hit_distance
+ * (scene.cu:134-241) -- one bounce of process_ray up to the hit (scene.cu:320-374) -- through
+ * the render's traversal kernel.  t_out[i] = closest distance (1e30 when nothing is hit),
+ * index_out[i] = primitive index (spheres first, then sphere_count + triangle; -1 = miss).
+ * With opts->collect_counters the traversal counters are returned in stats. */
+int rt_trace_rays(const rt_scene *scene, const rt_opts *opts, const float *rays, int32_t n,
+                  float *t_out, int32_t *index_out, rt_stats *stats);
 
 /* Replaces the bloom block of main (raytracing.cu:356-393, kernels :21-74): high-pass
  * (luminance > threshold), clamped box blur of `radius` horizontally then vertically,

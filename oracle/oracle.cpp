@@ -924,6 +924,34 @@ int orc_render_cpu_path_counted(const orc_scene *s, float *fb, int pass_limit, i
 }
 
 // raytracing.cu:21-74 with the launch parameters of :376-382.
+void orc_closest_hit(const orc_scene *s, const float *rays, int n, float *t_out, int32_t *index_out, orc_stats *st) {
+    Counters c;
+    const int sphere_count = (int)s->spheres.size();
+    for (int i = 0; i < n; i++) {
+        const float *r = rays + (size_t)i * 6;
+        const V3 o{r[0], r[1], r[2]}, d{r[3], r[4], r[5]};
+        float closest = 1e30f;                 // scene.cu:328-374, as process_ray
+        int index = -1;
+        for (int k = 0; k < sphere_count; k++) {
+            c.st++;
+            float t;
+            if (ray_sphere(s->spheres[k], o, d, closest, &t)) { closest = t; index = k; }
+        }
+        bvh_closest_hit(s, o, d, closest, index, c);
+        if (t_out) t_out[i] = closest;
+        if (index_out) index_out[i] = index;
+    }
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->live_segments = (uint64_t)n;
+        st->nodes_popped = c.pn;
+        st->internal_visits = c.iv;
+        st->triangle_tests = c.tt;
+        st->sphere_tests = c.st;
+        st->max_stack = c.max_stack;
+    }
+}
+
 void orc_bloom(float *fb, int w, int h, float threshold, int radius) {
     const int64_t n = (int64_t)w * h;
     std::vector<V3> img(n), bright(n), blur(n);

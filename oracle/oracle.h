@@ -87,6 +87,12 @@ int orc_render_cpu_path(const orc_scene *s, float *fb_out, int pass_limit, int t
 int orc_render_cpu_path_counted(const orc_scene *s, float *fb_out, int pass_limit, int threads,
                                 double *seconds, uint64_t *live_segments);
 
+/* Closest hit of n rays {o.xyz, d.xyz}: the sphere loop (scene.cu:338-372) then
+ * bvh_closest_hit_distance (scene.cu:134-241).  t_out = closest (1e30 if nothing is hit),
+ * index_out = primitive index or -1; stats (optional) gets Pn / Iv / Tt / sphere tests. */
+void orc_closest_hit(const orc_scene *s, const float *rays, int n, float *t_out, int32_t *index_out,
+                     orc_stats *stats);
+
 /* Post-process (raytracing.cu:21-74, 286-303). */
 void orc_bloom(float *fb, int width, int height, float threshold, int radius);
 void orc_tonemap(const float *fb, int width, int height, float exposure, int ray_count,

@@ -52,6 +52,7 @@ def lib():
         L.orc_render_gpu_semantics.argtypes = [P, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int]
         L.orc_render_pass_sums.argtypes = [P, C.c_int, C.c_int, C.c_int, P, C.c_int]
         L.orc_render_cpu_path.argtypes = [P, P, C.c_int, C.c_int, P]
+        L.orc_closest_hit.argtypes = [P, P, C.c_int, P, P, P]
         L.orc_bloom.argtypes = [P, C.c_int, C.c_int, C.c_float, C.c_int]
         L.orc_tonemap.argtypes = [P, C.c_int, C.c_int, C.c_float, C.c_int, P]
         L.orc_pcg_stream.argtypes = [C.c_uint32, C.c_int, P]
@@ -138,6 +139,15 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(lib().orc_last_error().decode())
         return out
+
+    def closest_hit(self, rays):
+        """Closest hit of rays (n, 6) {o.xyz, d.xyz}: (t, index, stats)."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        t = np.zeros(rays.shape[0], np.float32)
+        idx = np.zeros(rays.shape[0], np.int32)
+        st = OrcStats()
+        lib().orc_closest_hit(self.h, ptr(rays), rays.shape[0], ptr(t), ptr(idx), C.byref(st))
+        return t, idx, st.as_dict()
 
     def render_cpu_path(self, pass_limit=-1, threads=0):
         fb = np.zeros(self.pixels * 3, np.float32)
