@@ -175,7 +175,6 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 // do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
 template <bool SORTED, bool COUNT, bool FIRST>
 __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
-                                                       const uint32_t *__restrict__ idx,
                                                        const uint8_t *__restrict__ bkt,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
@@ -246,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
                         o = S.cam;
                         d = primary_dir(S, slot, pa);
                     } else {
-                        const float4 *rp = geo + (size_t)(SORTED ? idx[slot] : (uint32_t)slot) * 2;
+                        const float4 *rp = geo + (size_t)slot * 2;   // ray state is in slot order
                         const float4 r0 = rp[0];
                         const float2 r1 = *reinterpret_cast<const float2 *>(rp + 1);
                         o = v3(r0.x, r0.y, r0.z);
@@ -402,22 +401,25 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, 
 
 // Shading for the live slots (scene.cu:376-485): environment lookup on a miss, otherwise
 // emission + scatter; then the new ray state and its reorder bucket.  One lane per slot.
+// Ray state lives in slot order (the reorder moves it), so every access here is coalesced.  A
+// ray's radiance goes to acc[ray id] (pixel-major, what accumulation reads) when it terminates
+// or after the last bounce; with sort off slots are ray ids and tc doubles as acc.
 template <bool SORTED, bool COUNT, bool FIRST>
 __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
-                                                       float4 *__restrict__ tc, uint32_t *__restrict__ idx,
-                                                       uint8_t *__restrict__ bkt, const uint32_t *__restrict__ live_count,
-                                                       const float2 *__restrict__ hits, uint32_t seed_term,
+                                                       float4 *__restrict__ tc, const uint32_t *__restrict__ rid,
+                                                       float4 *__restrict__ acc, uint8_t *__restrict__ bkt,
+                                                       const uint32_t *__restrict__ live_count,
+                                                       const float2 *__restrict__ hits, uint32_t seed_term, int last,
                                                        Counters *__restrict__ ctr) {
     const int L = (int)__builtin_amdgcn_readfirstlane(*live_count);
     unsigned hit = 0, miss = 0, hit_sphere = 0;
     for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
         const int slot = base + threadIdx.x;
-        if (slot >= L || (!FIRST && bkt[slot] == kDead)) continue;
+        if (slot >= L || (!SORTED && !FIRST && bkt[slot] == kDead)) continue;
         Rng rng = pcg_seed((uint32_t)slot * 4137874753u + seed_term);   // raytracing.cu:89
         const float2 h = hits[slot];
         const float closest = h.x;
         const int index = __float_as_int(h.y);
-        const uint32_t ri = (SORTED && !FIRST) ? idx[slot] : (uint32_t)slot;
         V3 o, d, T, C;
         if (FIRST) {
             o = S.cam;
@@ -430,9 +432,8 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
             asm volatile("" : "+v"(tx), "+v"(ty), "+v"(tz));
             T = v3(tx, ty, tz);
             C = v3(0, 0, 0);
-            if (SORTED) idx[slot] = (uint32_t)slot;
         } else {
-            const float4 r0 = geo[(size_t)ri * 2], r1 = geo[(size_t)ri * 2 + 1], r2 = tc[ri];
+            const float4 r0 = geo[(size_t)slot * 2], r1 = geo[(size_t)slot * 2 + 1], r2 = tc[slot];
             o = v3(r0.x, r0.y, r0.z);
             d = v3(r0.w, r1.x, r1.y);
             T = v3(r1.z, r1.w, r2.x);
@@ -457,10 +458,20 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
             }
             scatter(d, normal, load_mat(S.mats + (size_t)S.mat_idx[index] * 3), rng, T, C, nd);
         }
-        geo[(size_t)ri * 2] = make_float4(no.x, no.y, no.z, nd.x);
-        geo[(size_t)ri * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
-        tc[ri] = make_float4(T.z, C.x, C.y, C.z);
-        bkt[slot] = (uint8_t)(is_black(T) ? kDead : bucket_of(no, nd, S.min_coord, S.inv_dim));
+        const bool dead = is_black(T);
+        const float4 tcv = make_float4(T.z, C.x, C.y, C.z);
+        if (!dead && !(SORTED && last)) {   // a terminated ray's geometry is never read again
+            geo[(size_t)slot * 2] = make_float4(no.x, no.y, no.z, nd.x);
+            geo[(size_t)slot * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
+        }
+        if (SORTED) {
+            if (dead || last) acc[FIRST ? (uint32_t)slot : rid[slot]] = tcv;
+            else tc[slot] = tcv;
+            if (!last) bkt[slot] = (uint8_t)(dead ? kDead : bucket_of(no, nd, S.min_coord, S.inv_dim));
+        } else {
+            tc[slot] = tcv;
+            bkt[slot] = (uint8_t)(dead ? kDead : bucket_of(no, nd, S.min_coord, S.inv_dim));
+        }
     }
     if (COUNT) {
         Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
@@ -556,13 +567,19 @@ __global__ __launch_bounds__(kBlock) void sort_scan_kernel(const uint32_t *__res
 }
 
 // Stable scatter: rounds of 256 consecutive slots; rank = earlier rounds + earlier waves +
-// earlier lanes holding the same bucket.
+// earlier lanes holding the same bucket.  Live rays move with their state (geometry, T/C, ray
+// id) so that the next bounce reads them in slot order; terminated rays (bucket 64, last in the
+// order) have already delivered their radiance and are dropped.  At bounce 0 slot = ray id.
+template <bool FIRST_SRC>
 __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__restrict__ bkt_in,
-                                                              const uint32_t *__restrict__ idx_in,
+                                                              const float4 *__restrict__ geo_in,
+                                                              const float4 *__restrict__ tc_in,
+                                                              const uint32_t *__restrict__ rid_in,
                                                               const uint32_t *__restrict__ live_count, int tiles,
                                                               const uint32_t *__restrict__ offsets,
                                                               const uint32_t *__restrict__ totals,
-                                                              uint8_t *__restrict__ bkt_out, uint32_t *__restrict__ idx_out) {
+                                                              float4 *__restrict__ geo_out, float4 *__restrict__ tc_out,
+                                                              uint32_t *__restrict__ rid_out) {
     const int n = (int)*live_count;
     if ((int)blockIdx.x * kSortTile >= n) return;
     __shared__ uint32_t run[kBuckets];
@@ -582,16 +599,26 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
         const int item = base + r * kBlock + threadIdx.x;
         const bool valid = item < n;
         const uint32_t b = valid ? bkt_in[item] : 0u;
-        const uint32_t ix = valid ? idx_in[item] : 0u;
+        const bool move = valid && b != kDead;
+        float4 g0 = make_float4(0, 0, 0, 0), g1 = g0, t = g0;
+        uint32_t id = 0;
+        if (move) {                     // issued before the ranking so the loads overlap it
+            g0 = geo_in[(size_t)item * 2];
+            g1 = geo_in[(size_t)item * 2 + 1];
+            t = tc_in[item];
+            id = FIRST_SRC ? (uint32_t)item : rid_in[item];
+        }
         const unsigned long long peers = match_bucket(b, valid);
         const uint32_t rank = rank_below(peers);
         if (valid && rank == 0) wcount[wave][b] = (uint32_t)__popcll(peers);
         __syncthreads();
-        if (valid) {
+        if (move) {
             uint32_t pos = run[b] + rank;
             for (int k = 0; k < wave; k++) pos += wcount[k][b];
-            idx_out[pos] = ix;
-            bkt_out[pos] = (uint8_t)b;
+            geo_out[(size_t)pos * 2] = g0;
+            geo_out[(size_t)pos * 2 + 1] = g1;
+            tc_out[pos] = t;
+            rid_out[pos] = id;
         }
         __syncthreads();
         if (threadIdx.x < kBuckets) {
@@ -721,9 +748,12 @@ bool is_leaf(const rt_bvh_node &nd) { return nd.child2 <= nd.child1; }   // scen
 // Device state of one in-flight pass: its own stream, ray state, reorder buffers and queues.
 struct PassCtx {
     hipStream_t stream = nullptr;
-    DevBuf<float4> geo, tc;           // ray state by ray index: 2 x float4 traversal part, {T.z, C}
-    DevBuf<uint32_t> idx[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
-    DevBuf<uint8_t> bkt[2];
+    // Ray state in slot order, ping-ponged by the reorder (sort off: one copy, slot = ray id):
+    // geo = 2 x float4 {o.xyz, d.x} {d.yz, T.xy}, tc = {T.z, C.xyz}, rid = ray id.  acc[ray id]
+    // receives a ray's {T.z, C} when it terminates or after the last bounce (sort on only).
+    DevBuf<float4> geo[2], tc[2], acc;
+    DevBuf<uint32_t> rid[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
+    DevBuf<uint8_t> bkt;
     DevBuf<float2> hits;
     DevBuf<float> psum;               // this pass's per-pixel sums (when the caller gives no buffer)
     hipEvent_t fb_done = nullptr;     // recorded after this context last added into the framebuffer
@@ -845,7 +875,7 @@ struct rt_renderer {
         const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
         // than half of the free device memory holds (1080p: ~2.9 GB per context).
-        const size_t ctx_bytes = (size_t)max_rays * (32 + 16 + 8 + 8 + (sort ? 10 : 0)) +
+        const size_t ctx_bytes = (size_t)max_rays * (sort ? 2 * (32 + 16 + 4) + 16 + 1 + 8 : 32 + 16 + 1 + 8) +
                                  (size_t)trace_blocks * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
         size_t mem_free = 0, mem_total = 0;
         HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
@@ -854,14 +884,14 @@ struct rt_renderer {
         const int inflight = nctx;
         for (int k = 0; k < inflight; k++) {
             PassCtx &c = ctx[k];
-            if ((rc = c.geo.alloc((size_t)max_rays * 2))) return rc;
-            if ((rc = c.tc.alloc((size_t)max_rays))) return rc;
-            for (int q = 0; q < 2; q++) {
-                if ((rc = c.idx[q].alloc((size_t)max_rays))) return rc;
-                if ((rc = c.bkt[q].alloc((size_t)max_rays))) return rc;
-                if (!sort) break;
+            for (int q = 0; q < (sort ? 2 : 1); q++) {
+                if ((rc = c.geo[q].alloc((size_t)max_rays * 2))) return rc;
+                if ((rc = c.tc[q].alloc((size_t)max_rays))) return rc;
+                if (sort && (rc = c.rid[q].alloc((size_t)max_rays))) return rc;
             }
+            if ((rc = c.bkt.alloc((size_t)max_rays))) return rc;
             if (sort) {
+                if ((rc = c.acc.alloc((size_t)max_rays))) return rc;
                 if ((rc = c.sort_counts.alloc((size_t)kBuckets * tiles))) return rc;
                 if ((rc = c.sort_offsets.alloc((size_t)kBuckets * tiles))) return rc;
                 if ((rc = c.sort_totals.alloc(kBuckets))) return rc;
@@ -920,12 +950,14 @@ struct rt_renderer {
             HIPCHK(hipEventRecord(e0, st));
             const uint32_t *lv = c.live.p + b;
             uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
+            const bool last = b + 1 == bounces;
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
         hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,        \
-                           c.geo.p, c.idx[cur].p, c.bkt[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);              \
+                           c.geo[cur].p, c.bkt.p, lv, q, c.hits.p, c.overflow.p, ctr.p);                          \
         hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST>), dim3(sgrid), dim3(kBlock), 0, st, ds, pa,        \
-                           c.geo.p, c.tc.p, c.idx[cur].p, c.bkt[cur].p, lv, c.hits.p, seed_term, ctr.p);         \
+                           c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p, seed_term,   \
+                           (int)last, ctr.p);                                                                    \
     } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
     do {                                                                                                         \
@@ -944,12 +976,18 @@ struct rt_renderer {
                 hipEvent_t s0 = c.event(), s1 = c.event();
                 if (!s0 || !s1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
                 HIPCHK(hipEventRecord(s0, st));
-                hipLaunchKernelGGL(sort_hist_kernel, dim3(tiles), dim3(kBlock), 0, st, c.bkt[cur].p, lv, tiles,
+                hipLaunchKernelGGL(sort_hist_kernel, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, lv, tiles,
                                    c.sort_counts.p);
                 hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, lv, tiles,
                                    c.sort_offsets.p, c.sort_totals.p, c.live.p + b + 1);
-                hipLaunchKernelGGL(sort_scatter_kernel, dim3(tiles), dim3(kBlock), 0, st, c.bkt[cur].p, c.idx[cur].p,
-                                   lv, tiles, c.sort_offsets.p, c.sort_totals.p, c.bkt[1 - cur].p, c.idx[1 - cur].p);
+                if (b == 0)
+                    hipLaunchKernelGGL(sort_scatter_kernel<true>, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p);
+                else
+                    hipLaunchKernelGGL(sort_scatter_kernel<false>, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventRecord(s1, st));
                 cur = 1 - cur;
@@ -961,7 +999,7 @@ struct rt_renderer {
             HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
         } else {
             hipLaunchKernelGGL(accumulate_kernel, dim3((unsigned)((pixels + kAccPixels - 1) / kAccPixels)), dim3(kBlock),
-                               0, st, c.tc.p, rtc, (int)pixels, sums);
+                               0, st, sort ? c.acc.p : c.tc[0].p, rtc, (int)pixels, sums);
         }
         HIPCHK(hipGetLastError());
         return RT_OK;
@@ -998,10 +1036,10 @@ struct rt_renderer {
         const int tgrid = std::min(blocks_for(n), trace_blocks);
         if (counters)
             hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               nullptr, bkt.p, live.p, queue.p, hits.p, overflow.p, ctr.p);
+                               bkt.p, live.p, queue.p, hits.p, overflow.p, ctr.p);
         else
             hipLaunchKernelGGL((trace_kernel<false, false, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               nullptr, bkt.p, live.p, queue.p, hits.p, overflow.p, ctr.p);
+                               bkt.p, live.p, queue.p, hits.p, overflow.p, ctr.p);
         HIPCHK(hipGetLastError());
         std::vector<float2> h((size_t)n);
         HIPCHK(hipMemcpyAsync(h.data(), hits.p, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, s0));
