@@ -48,7 +48,7 @@ namespace {
 #define RT_INFLIGHT 12
 #endif
 #ifndef RT_TRACE_OCC
-#define RT_TRACE_OCC 75
+#define RT_TRACE_OCC 40
 #endif
 #ifndef RT_QUEUES
 #define RT_QUEUES 8
@@ -173,8 +173,13 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 // chunks of slots from a device queue (one atomic per chunk) and hands a new slot to a lane
 // as soon as that lane's ray is done, so incoherent rays of very different traversal lengths
 // do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
+#ifdef RT_TRACE_WPE
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, 8)))
+#else
+#define RT_TRACE_ATTR
+#endif
 template <bool SORTED, bool COUNT, bool FIRST>
-__global__ __launch_bounds__(kBlock) void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
+__global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint8_t *__restrict__ bkt,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
