@@ -235,8 +235,16 @@ def main():
             achieved = bytes_total / elapsed / 1e9 if elapsed > 0 else 0.0
             per_launch = bytes_launch / (ms_launch / 1e3) / 1e9 if ms_launch > 0 else 0.0
             traffic = load_pmc(workload)
+            # measured HBM-side bytes (rocprofv3 PMC, per trace+shade launch) over the same launches
+            hbm_gbs = traffic * launches / elapsed / 1e9 if traffic and elapsed > 0 else None
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "hbm_measured_gbs": round(hbm_gbs, 1) if hbm_gbs else None,
+                    "hbm_measured_frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
+                    "note": "achieved/frac: SURVEY.md 8(d) logical bytes (every BVH node and triangle fetch counted, "
+                            "cache-inclusive) over the render wall; frac > 1 means the traversal working set is "
+                            "served by L2/Infinity Cache. traffic: measured L2->fabric bytes per trace+shade launch "
+                            "(profiles/pmc_process_kernel.json); hbm_measured_*: that traffic over the same wall",
                     "kernel": "process (trace_kernel + shade_kernel per bounce)",
                     "bytes_per_launch": int(bytes_launch), "ms_per_launch": round(ms_launch, 4),
                     "achieved_per_launch_events": round(per_launch, 1),
