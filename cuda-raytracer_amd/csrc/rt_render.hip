@@ -41,6 +41,9 @@ namespace {
 #ifndef RT_REFILL
 #define RT_REFILL 16
 #endif
+#ifndef RT_REFILL_FIRST
+#define RT_REFILL_FIRST 16
+#endif
 #ifndef RT_CHUNK_MAX
 #define RT_CHUNK_MAX 128
 #endif
@@ -63,6 +66,7 @@ constexpr int kCtrSlots = 64;       // striped copies of the work counters
 constexpr int kChunkMax = RT_CHUNK_MAX; // slots a wave takes from the trace queue per atomic...
 constexpr int kChunkMin = 64;        // ...shrunk so that every wave gets ~4 chunks when few rays live
 constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are idle
+constexpr int kRefillFirst = RT_REFILL_FIRST;   // same at bounce 0 (primary-ray setup is dearer)
 constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffer set each)
 constexpr int kTraceOccPct = RT_TRACE_OCC; // % of the resident trace workgroups the persistent grid uses
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
@@ -114,15 +118,33 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 // is needed (trace and shade of bounce 0) instead of being written out and read back.  Ray i
 // of a pass is slot i at bounce 0.  Ray state afterwards: geo[2 i .. 2 i + 1] = {o.xyz, d.x},
 // {d.yz, T.xy} (what traversal reads) and tc[i] = {T.z, C.xyz} (what accumulation reads).
+// n / d for n < 2^31 as a multiply-high and a shift (Granlund-Montgomery: m = ceil(2^(31+l)/d),
+// l = ceil(log2 d)); l = 0 means d = 1.
+struct FastDiv {
+    uint32_t m = 0;
+    int l = 0;
+    static FastDiv of(uint32_t d) {
+        FastDiv f;
+        if (d > 1) {
+            f.l = 32 - __builtin_clz(d - 1);
+            f.m = (uint32_t)((((uint64_t)1 << (31 + f.l)) + d - 1) / d);
+        }
+        return f;
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const { return l == 0 ? n : (__umulhi(n, m) >> (l - 1)); }
+};
+
 struct PassArgs {
     int rtc;                          // rays per pixel this pass
     uint32_t gen_seed_term;           // 709579 * remaining (scene.cu:81)
+    FastDiv by_rtc, by_width;         // ray index -> pixel -> row
 };
 
 __device__ __forceinline__ V3 primary_dir(const DevScene &S, int i, const PassArgs &pa) {
     Rng rng = pcg_seed((uint32_t)i * 0x85810BEAu + pa.gen_seed_term);   // 298592570346 mod 2^32
-    const int pixel = i / pa.rtc;
-    const int x = pixel % S.width, y = pixel / S.width;
+    const uint32_t pixel = pa.by_rtc.div((uint32_t)i);
+    const uint32_t yy = pa.by_width.div(pixel);
+    const int x = (int)(pixel - yy * (uint32_t)S.width), y = (int)yy;
     const float xc = (x + random01(rng)) * S.inv_w;
     const float yc = (y + random01(rng)) * S.inv_h;
     return normalise(S.tl + xc * S.sr - yc * S.su);
@@ -130,6 +152,7 @@ __device__ __forceinline__ V3 primary_dir(const DevScene &S, int i, const PassAr
 
 // ---------------------------------------------------------------- traversal
 typedef float f2 __attribute__((ext_vector_type(2)));
+
 
 // Both children's slab tests (ray_aabb_intersection, scene.cu:109-132) on the interleaved node
 // record {lx0 lx1 ly0 ly1} {lz0 lz1 hx0 hx1} {hy0 hy1 hz0 hz1}: the plane distances of the two
@@ -215,7 +238,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     while (true) {
         // ---- refill idle lanes (wave-uniform control flow)
         unsigned long long idle = __ballot(slot < 0);
-        if (!exhausted && __popcll(idle) >= kRefill) {
+        if (!exhausted && __popcll(idle) >= (FIRST ? kRefillFirst : kRefill)) {
             PROF(6, 1);
             bool fresh = false;
             while (idle && !exhausted) {
@@ -947,7 +970,7 @@ struct rt_renderer {
         hipStream_t st = c.stream;
         int cur = 0;
         hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1, c.queue.p);
-        const PassArgs pa{rtc, 709579u * (uint32_t)remaining};
+        const PassArgs pa{rtc, 709579u * (uint32_t)remaining, FastDiv::of((uint32_t)rtc), FastDiv::of((uint32_t)width)};
         for (int b = 0; b < bounces; b++) {
             const uint32_t seed_term = 279220567u * (uint32_t)(remaining * 20 + b);
             hipEvent_t e0 = c.event(), e1 = c.event();
@@ -1037,7 +1060,7 @@ struct rt_renderer {
         const uint32_t nn = (uint32_t)n;
         HIPCHK(hipMemcpyAsync(live.p, &nn, sizeof(nn), hipMemcpyHostToDevice, s0));
         HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, s0));
-        const PassArgs pa{1, 0u};
+        const PassArgs pa{1, 0u, FastDiv::of(1), FastDiv::of((uint32_t)width)};
         const int tgrid = std::min(blocks_for(n), trace_blocks);
         if (counters)
             hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
