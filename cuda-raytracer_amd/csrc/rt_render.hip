@@ -848,13 +848,34 @@ struct rt_renderer {
         HIPCHK(hipEventCreate(&t_end));
         hipStream_t s0 = stream();
         int rc;
-        // Child-pair node records (see file header).  Internal nodes keep the reference's
-        // depth-first order, so a subtree's records stay contiguous.
+        // Child-pair node records.  Record numbering: the two children of a node get adjacent
+        // records (an even/odd pair, one 128-B line), so stepping into one child brings in its
+        // sibling's record too, which the stack usually visits next; pairs are handed out in
+        // depth-first order so a subtree's records stay close.  Layout only: the traversal
+        // order is unchanged.
         const int nn = sc->bvh_node_count;
         std::vector<int> rec(nn, -1);
         int nrec = 0;
-        for (int i = 0; i < nn; i++)
-            if (!is_leaf(sc->bvh[i])) rec[i] = nrec++;
+        if (nn > 0 && !is_leaf(sc->bvh[0])) {
+            rec[0] = 0;
+            nrec = 2;                   // record 1: padding, the root has no sibling
+            std::vector<int> todo{0};
+            int visited = 0;
+            while (!todo.empty()) {
+                const int i = todo.back();
+                todo.pop_back();
+                if (++visited > nn) return rtamd::fail(RT_E_INVALID, "BVH is not a tree");
+                const rt_bvh_node &nd = sc->bvh[i];
+                if (nd.child1 < 0 || nd.child2 >= nn || nd.child1 >= nn || nd.child2 < 0)
+                    return rtamd::fail(RT_E_INVALID, "BVH child index out of range");
+                const bool in1 = !is_leaf(sc->bvh[nd.child1]), in2 = !is_leaf(sc->bvh[nd.child2]);
+                if (in1) rec[nd.child1] = nrec;
+                if (in2) rec[nd.child2] = nrec + 1;
+                if (in1 || in2) nrec += 2;
+                if (in2) todo.push_back(nd.child2);   // child1's subtree first (depth-first)
+                if (in1) todo.push_back(nd.child1);
+            }
+        }
         std::vector<int2> big_h;
         auto ref_of = [&](int c) -> uint32_t {
             const rt_bvh_node &nd = sc->bvh[c];
@@ -868,7 +889,6 @@ struct rt_renderer {
         for (int i = 0; i < nn; i++) {
             if (rec[i] < 0) continue;
             const rt_bvh_node &nd = sc->bvh[i];
-            if (nd.child1 < 0 || nd.child2 >= nn) return rtamd::fail(RT_E_INVALID, "BVH child index out of range");
             const rt_bvh_node &l = sc->bvh[nd.child1], &r = sc->bvh[nd.child2];
             float4 *q = &rec_h[(size_t)rec[i] * 4];
             // the two children's bounds interleaved per plane, so one packed-fp32 op handles both
