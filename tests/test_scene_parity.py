@@ -24,6 +24,19 @@ def test_loader_arrays_identical(name, bvh):
         assert a[k].tobytes() == b[k].tobytes(), k
 
 
+@pytest.mark.parametrize("threads", ["1", "2", "3", "16"])
+def test_bvh_build_independent_of_threads(threads, monkeypatch):
+    """The parallel BVH build (subtrees and chunked scans on threads) emits the serial
+    reference build's node array and triangle order for any thread count."""
+    monkeypatch.setenv("RT_BVH_THREADS", threads)
+    for name in ("teapot", "lamp_available"):
+        path = os.path.join(R.ASSETS, name + ".scene")
+        a = O.OracleScene(path).arrays()
+        b = R.Scene(path).arrays()
+        for k in ("bvh", "triangles", "material_indices"):
+            assert a[k].tobytes() == b[k].tobytes(), (name, threads, k)
+
+
 def test_image_override_and_camera():
     path = os.path.join(R.ASSETS, "teapot.scene")
     a = O.OracleScene(path, image=(321, 123, 45, 6), exposure=0.25).arrays()["camera"]
