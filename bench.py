@@ -213,7 +213,7 @@ def main():
         counted = {}
         run_steps(steps, counted)
         counted = {k: int(v) for k, v in counted.items() if isinstance(v, int)}
-        counted["dead_slot_bytes"] = 0 if sort else counted["dead_slots"]
+        counted["dead_slot_bytes"] = 0   # terminated slots are never visited (reorder or live list)
         ren.set_counters(False)
     bytes_total = segment_bytes(counted, scene.view.sphere_count) if counted else 0.0
     launches = my_passes * bounces

@@ -203,7 +203,7 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #endif
 template <bool SORTED, bool COUNT, bool FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
-                                                       const uint8_t *__restrict__ bkt,
+                                                       const uint32_t *__restrict__ list,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr) {
@@ -265,15 +265,15 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 idle &= ~took;
             }
             if (fresh) {
-                if (!FIRST && !SORTED && bkt[slot] == kDead) {
-                    slot = -1;          // no_sort: terminated rays stay in place
-                } else {
+                {
                     nlive++;
                     if (FIRST) {
                         o = S.cam;
                         d = primary_dir(S, slot, pa);
                     } else {
-                        const float4 *rp = geo + (size_t)slot * 2;   // ray state is in slot order
+                        // ray state is in slot order; with sort off, `list` holds the live slots
+                        const uint32_t rs = (!SORTED && list) ? list[slot] : (uint32_t)slot;
+                        const float4 *rp = geo + (size_t)rs * 2;
                         const float4 r0 = rp[0];
                         const float2 r1 = *reinterpret_cast<const float2 *>(rp + 1);
                         o = v3(r0.x, r0.y, r0.z);
@@ -436,16 +436,19 @@ template <bool SORTED, bool COUNT, bool FIRST>
 __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
                                                        float4 *__restrict__ tc, const uint32_t *__restrict__ rid,
                                                        float4 *__restrict__ acc, uint8_t *__restrict__ bkt,
+                                                       const uint32_t *__restrict__ list,
                                                        const uint32_t *__restrict__ live_count,
                                                        const float2 *__restrict__ hits, uint32_t seed_term, int last,
                                                        Counters *__restrict__ ctr) {
     const int L = (int)__builtin_amdgcn_readfirstlane(*live_count);
     unsigned hit = 0, miss = 0, hit_sphere = 0;
     for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
-        const int slot = base + threadIdx.x;
-        if (slot >= L || (!SORTED && !FIRST && bkt[slot] == kDead)) continue;
+        const int k = base + threadIdx.x;
+        if (k >= L) continue;
+        // with sort off, position k of the live list holds slot list[k] (bounce 0: all slots)
+        const int slot = (!SORTED && !FIRST) ? (int)list[k] : k;
         Rng rng = pcg_seed((uint32_t)slot * 4137874753u + seed_term);   // raytracing.cu:89
-        const float2 h = hits[slot];
+        const float2 h = hits[k];
         const float closest = h.x;
         const int index = __float_as_int(h.y);
         V3 o, d, T, C;
@@ -512,12 +515,36 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
     }
 }
 
-__global__ void fill_live_kernel(uint32_t *__restrict__ live, uint32_t n, int count, uint32_t *__restrict__ queue) {
+// live[0] = n; the later counts are n (sort on: the reorder's scan overwrites them) or 0 (sort
+// off: the live-list compaction counts into them).
+__global__ void fill_live_kernel(uint32_t *__restrict__ live, uint32_t n, int count, uint32_t later,
+                                 uint32_t *__restrict__ queue) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < count) live[i] = n;
+    if (i < count) live[i] = i == 0 ? n : later;
     for (int k = i; k < count * kQueues * kQueueStride; k += blockDim.x) queue[k] = 0;
 }
 
+
+// Sort off: the slots still live after a bounce, gathered from the current live list (bounce 0:
+// all slots) so the next bounce visits only them.  The list order is irrelevant (a slot keeps
+// its seed and state), so a wave appends its live slots with one atomic.
+__global__ __launch_bounds__(kBlock) void compact_live_kernel(const uint32_t *__restrict__ list_in,
+                                                              const uint8_t *__restrict__ bkt,
+                                                              const uint32_t *__restrict__ live_count,
+                                                              uint32_t *__restrict__ list_out,
+                                                              uint32_t *__restrict__ live_next) {
+    const uint32_t L = *live_count;
+    for (uint32_t base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
+        const uint32_t k = base + threadIdx.x;
+        const uint32_t s = k < L ? (list_in ? list_in[k] : k) : 0u;
+        const bool alive = k < L && bkt[s] != kDead;
+        const unsigned long long m = __ballot(alive);
+        uint32_t at = 0;
+        if (lane_id() == 0 && m) at = atomicAdd(live_next, (uint32_t)__popcll(m));
+        at = __shfl(at, 0);
+        if (alive) list_out[at + rank_below(m)] = s;
+    }
+}
 
 // ---------------------------------------------------------------- stable 65-bucket reorder
 // Equivalent to cub::DeviceRadixSort::SortPairs on the reference keys (raytracing.cu:238-247).
@@ -782,6 +809,7 @@ struct PassCtx {
     DevBuf<float4> geo[2], tc[2], acc;
     DevBuf<uint32_t> rid[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
     DevBuf<uint8_t> bkt;
+    DevBuf<uint32_t> list[2];         // sort off: live slots of the current / next bounce
     DevBuf<float2> hits;
     DevBuf<float> psum;               // this pass's per-pixel sums (when the caller gives no buffer)
     hipEvent_t fb_done = nullptr;     // recorded after this context last added into the framebuffer
@@ -938,6 +966,9 @@ struct rt_renderer {
                 if (sort && (rc = c.rid[q].alloc((size_t)max_rays))) return rc;
             }
             if ((rc = c.bkt.alloc((size_t)max_rays))) return rc;
+            if (!sort)
+                for (int q = 0; q < 2; q++)
+                    if ((rc = c.list[q].alloc((size_t)max_rays))) return rc;
             if (sort) {
                 if ((rc = c.acc.alloc((size_t)max_rays))) return rc;
                 if ((rc = c.sort_counts.alloc((size_t)kBuckets * tiles))) return rc;
@@ -989,7 +1020,9 @@ struct rt_renderer {
         const int sgrid = std::min(grid, cus * 8);
         hipStream_t st = c.stream;
         int cur = 0;
-        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1, c.queue.p);
+        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1,
+                           sort ? (uint32_t)n : 0u, c.queue.p);
+        int lcur = 0;                   // sort off: live list of the current bounce
         const PassArgs pa{rtc, 709579u * (uint32_t)remaining, FastDiv::of((uint32_t)rtc), FastDiv::of((uint32_t)width)};
         for (int b = 0; b < bounces; b++) {
             const uint32_t seed_term = 279220567u * (uint32_t)(remaining * 20 + b);
@@ -1002,10 +1035,10 @@ struct rt_renderer {
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
         hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,        \
-                           c.geo[cur].p, c.bkt.p, lv, q, c.hits.p, c.overflow.p, ctr.p);                          \
+                           c.geo[cur].p, c.list[lcur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                   \
         hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST>), dim3(sgrid), dim3(kBlock), 0, st, ds, pa,        \
-                           c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p, seed_term,   \
-                           (int)last, ctr.p);                                                                    \
+                           c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, c.list[lcur].p, lv,        \
+                           c.hits.p, seed_term, (int)last, ctr.p);                                               \
     } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
     do {                                                                                                         \
@@ -1020,6 +1053,12 @@ struct rt_renderer {
 #undef RT_PROCESS3
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(e1, st));
+            if (!sort && b + 1 != bounces) {
+                hipLaunchKernelGGL(compact_live_kernel, dim3(sgrid), dim3(kBlock), 0, st, b == 0 ? nullptr : c.list[lcur].p,
+                                   c.bkt.p, lv, c.list[1 - lcur].p, c.live.p + b + 1);
+                HIPCHK(hipGetLastError());
+                lcur = 1 - lcur;
+            }
             if (sort && b + 1 != bounces) {
                 hipEvent_t s0 = c.event(), s1 = c.event();
                 if (!s0 || !s1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
@@ -1067,15 +1106,13 @@ struct rt_renderer {
             g[(size_t)i * 2 + 1] = make_float4(r[4], r[5], 1.0f, 1.0f);
         }
         DevBuf<float4> geo;
-        DevBuf<uint8_t> bkt;
         DevBuf<uint32_t> live, queue, overflow;
         DevBuf<float2> hits;
         int rc;
         if ((rc = geo.upload(g.data(), g.size(), s0))) return rc;
-        if ((rc = bkt.alloc((size_t)n)) || (rc = live.alloc(1)) || (rc = queue.alloc((size_t)kQueues * kQueueStride)) ||
+        if ((rc = live.alloc(1)) || (rc = queue.alloc((size_t)kQueues * kQueueStride)) ||
             (rc = hits.alloc((size_t)n)) || (rc = overflow.alloc((size_t)trace_blocks * kBlock * 2 * (kStackMax - kStackLds))))
             return rc;
-        HIPCHK(hipMemsetAsync(bkt.p, 0, (size_t)n, s0));
         HIPCHK(hipMemsetAsync(queue.p, 0, queue.n * sizeof(uint32_t), s0));
         const uint32_t nn = (uint32_t)n;
         HIPCHK(hipMemcpyAsync(live.p, &nn, sizeof(nn), hipMemcpyHostToDevice, s0));
@@ -1084,10 +1121,10 @@ struct rt_renderer {
         const int tgrid = std::min(blocks_for(n), trace_blocks);
         if (counters)
             hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               bkt.p, live.p, queue.p, hits.p, overflow.p, ctr.p);
+                               nullptr, live.p, queue.p, hits.p, overflow.p, ctr.p);
         else
             hipLaunchKernelGGL((trace_kernel<false, false, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               bkt.p, live.p, queue.p, hits.p, overflow.p, ctr.p);
+                               nullptr, live.p, queue.p, hits.p, overflow.p, ctr.p);
         HIPCHK(hipGetLastError());
         std::vector<float2> h((size_t)n);
         HIPCHK(hipMemcpyAsync(h.data(), hits.p, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, s0));
