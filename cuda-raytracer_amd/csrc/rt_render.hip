@@ -203,7 +203,6 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #endif
 template <bool SORTED, bool COUNT, bool FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
-                                                       const uint32_t *__restrict__ list,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr) {
@@ -271,9 +270,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                         o = S.cam;
                         d = primary_dir(S, slot, pa);
                     } else {
-                        // ray state is in slot order; with sort off, `list` holds the live slots
-                        const uint32_t rs = (!SORTED && list) ? list[slot] : (uint32_t)slot;
-                        const float4 *rp = geo + (size_t)rs * 2;
+                        const float4 *rp = geo + (size_t)slot * 2;   // ray state is in slot order
                         const float4 r0 = rp[0];
                         const float2 r1 = *reinterpret_cast<const float2 *>(rp + 1);
                         o = v3(r0.x, r0.y, r0.z);
@@ -431,24 +428,24 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 // emission + scatter; then the new ray state and its reorder bucket.  One lane per slot.
 // Ray state lives in slot order (the reorder moves it), so every access here is coalesced.  A
 // ray's radiance goes to acc[ray id] (pixel-major, what accumulation reads) when it terminates
-// or after the last bounce; with sort off slots are ray ids and tc doubles as acc.
+// or after the last bounce.
 template <bool SORTED, bool COUNT, bool FIRST>
 __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
                                                        float4 *__restrict__ tc, const uint32_t *__restrict__ rid,
                                                        float4 *__restrict__ acc, uint8_t *__restrict__ bkt,
-                                                       const uint32_t *__restrict__ list,
                                                        const uint32_t *__restrict__ live_count,
                                                        const float2 *__restrict__ hits, uint32_t seed_term, int last,
                                                        Counters *__restrict__ ctr) {
     const int L = (int)__builtin_amdgcn_readfirstlane(*live_count);
     unsigned hit = 0, miss = 0, hit_sphere = 0;
     for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
-        const int k = base + threadIdx.x;
-        if (k >= L) continue;
-        // with sort off, position k of the live list holds slot list[k] (bounce 0: all slots)
-        const int slot = (!SORTED && !FIRST) ? (int)list[k] : k;
-        Rng rng = pcg_seed((uint32_t)slot * 4137874753u + seed_term);   // raytracing.cu:89
-        const float2 h = hits[k];
+        const int slot = base + threadIdx.x;
+        if (slot >= L) continue;
+        // The seed follows the reference's slot (raytracing.cu:89): the position with sort on;
+        // with sort off a ray keeps its original slot, which is its ray id.
+        const uint32_t seed_slot = (SORTED || FIRST) ? (uint32_t)slot : rid[slot];
+        Rng rng = pcg_seed(seed_slot * 4137874753u + seed_term);
+        const float2 h = hits[slot];
         const float closest = h.x;
         const int index = __float_as_int(h.y);
         V3 o, d, T, C;
@@ -491,18 +488,13 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
         }
         const bool dead = is_black(T);
         const float4 tcv = make_float4(T.z, C.x, C.y, C.z);
-        if (!dead && !(SORTED && last)) {   // a terminated ray's geometry is never read again
+        if (!dead && !last) {           // a terminated ray's geometry is never read again
             geo[(size_t)slot * 2] = make_float4(no.x, no.y, no.z, nd.x);
             geo[(size_t)slot * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
         }
-        if (SORTED) {
-            if (dead || last) acc[FIRST ? (uint32_t)slot : rid[slot]] = tcv;
-            else tc[slot] = tcv;
-            if (!last) bkt[slot] = (uint8_t)(dead ? kDead : bucket_of(no, nd, S.min_coord, S.inv_dim));
-        } else {
-            tc[slot] = tcv;
-            bkt[slot] = (uint8_t)(dead ? kDead : bucket_of(no, nd, S.min_coord, S.inv_dim));
-        }
+        if (dead || last) acc[FIRST ? (uint32_t)slot : rid[slot]] = tcv;
+        else tc[slot] = tcv;
+        if (!last) bkt[slot] = (uint8_t)(dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u));
     }
     if (COUNT) {
         Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
@@ -525,24 +517,40 @@ __global__ void fill_live_kernel(uint32_t *__restrict__ live, uint32_t n, int co
 }
 
 
-// Sort off: the slots still live after a bounce, gathered from the current live list (bounce 0:
-// all slots) so the next bounce visits only them.  The list order is irrelevant (a slot keeps
-// its seed and state), so a wave appends its live slots with one atomic.
-__global__ __launch_bounds__(kBlock) void compact_live_kernel(const uint32_t *__restrict__ list_in,
-                                                              const uint8_t *__restrict__ bkt,
+// Sort off: the rays still live after a bounce move (with their state, like the reorder's
+// scatter) to the front of the next buffers, so the next bounce visits only them, in slot
+// order.  Their order there is irrelevant: a ray keeps its seed slot (its ray id) and its
+// state, so a wave appends its live rays with one atomic.
+__global__ __launch_bounds__(kBlock) void compact_live_kernel(const uint8_t *__restrict__ bkt,
+                                                              const float4 *__restrict__ geo_in,
+                                                              const float4 *__restrict__ tc_in,
+                                                              const uint32_t *__restrict__ rid_in,
                                                               const uint32_t *__restrict__ live_count,
-                                                              uint32_t *__restrict__ list_out,
-                                                              uint32_t *__restrict__ live_next) {
+                                                              float4 *__restrict__ geo_out, float4 *__restrict__ tc_out,
+                                                              uint32_t *__restrict__ rid_out,
+                                                              uint32_t *__restrict__ live_next, int first) {
     const uint32_t L = *live_count;
     for (uint32_t base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
         const uint32_t k = base + threadIdx.x;
-        const uint32_t s = k < L ? (list_in ? list_in[k] : k) : 0u;
-        const bool alive = k < L && bkt[s] != kDead;
+        const bool alive = k < L && bkt[k] != kDead;
+        float4 g0 = make_float4(0, 0, 0, 0), g1 = g0, t = g0;
+        uint32_t id = 0;
+        if (alive) {
+            g0 = geo_in[(size_t)k * 2];
+            g1 = geo_in[(size_t)k * 2 + 1];
+            t = tc_in[k];
+            id = first ? k : rid_in[k];
+        }
         const unsigned long long m = __ballot(alive);
         uint32_t at = 0;
         if (lane_id() == 0 && m) at = atomicAdd(live_next, (uint32_t)__popcll(m));
-        at = __shfl(at, 0);
-        if (alive) list_out[at + rank_below(m)] = s;
+        at = __shfl(at, 0) + rank_below(m);
+        if (alive) {
+            geo_out[(size_t)at * 2] = g0;
+            geo_out[(size_t)at * 2 + 1] = g1;
+            tc_out[at] = t;
+            rid_out[at] = id;
+        }
     }
 }
 
@@ -809,7 +817,6 @@ struct PassCtx {
     DevBuf<float4> geo[2], tc[2], acc;
     DevBuf<uint32_t> rid[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
     DevBuf<uint8_t> bkt;
-    DevBuf<uint32_t> list[2];         // sort off: live slots of the current / next bounce
     DevBuf<float2> hits;
     DevBuf<float> psum;               // this pass's per-pixel sums (when the caller gives no buffer)
     hipEvent_t fb_done = nullptr;     // recorded after this context last added into the framebuffer
@@ -951,7 +958,7 @@ struct rt_renderer {
         const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
         // than half of the free device memory holds (1080p: ~2.9 GB per context).
-        const size_t ctx_bytes = (size_t)max_rays * (sort ? 2 * (32 + 16 + 4) + 16 + 1 + 8 : 32 + 16 + 1 + 8) +
+        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8) +
                                  (size_t)trace_blocks * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
         size_t mem_free = 0, mem_total = 0;
         HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
@@ -960,17 +967,14 @@ struct rt_renderer {
         const int inflight = nctx;
         for (int k = 0; k < inflight; k++) {
             PassCtx &c = ctx[k];
-            for (int q = 0; q < (sort ? 2 : 1); q++) {
+            for (int q = 0; q < 2; q++) {
                 if ((rc = c.geo[q].alloc((size_t)max_rays * 2))) return rc;
                 if ((rc = c.tc[q].alloc((size_t)max_rays))) return rc;
-                if (sort && (rc = c.rid[q].alloc((size_t)max_rays))) return rc;
+                if ((rc = c.rid[q].alloc((size_t)max_rays))) return rc;
             }
             if ((rc = c.bkt.alloc((size_t)max_rays))) return rc;
-            if (!sort)
-                for (int q = 0; q < 2; q++)
-                    if ((rc = c.list[q].alloc((size_t)max_rays))) return rc;
+            if ((rc = c.acc.alloc((size_t)max_rays))) return rc;
             if (sort) {
-                if ((rc = c.acc.alloc((size_t)max_rays))) return rc;
                 if ((rc = c.sort_counts.alloc((size_t)kBuckets * tiles))) return rc;
                 if ((rc = c.sort_offsets.alloc((size_t)kBuckets * tiles))) return rc;
                 if ((rc = c.sort_totals.alloc(kBuckets))) return rc;
@@ -1022,7 +1026,6 @@ struct rt_renderer {
         int cur = 0;
         hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1,
                            sort ? (uint32_t)n : 0u, c.queue.p);
-        int lcur = 0;                   // sort off: live list of the current bounce
         const PassArgs pa{rtc, 709579u * (uint32_t)remaining, FastDiv::of((uint32_t)rtc), FastDiv::of((uint32_t)width)};
         for (int b = 0; b < bounces; b++) {
             const uint32_t seed_term = 279220567u * (uint32_t)(remaining * 20 + b);
@@ -1035,10 +1038,10 @@ struct rt_renderer {
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
         hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,        \
-                           c.geo[cur].p, c.list[lcur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                   \
+                           c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                                   \
         hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST>), dim3(sgrid), dim3(kBlock), 0, st, ds, pa,        \
-                           c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, c.list[lcur].p, lv,        \
-                           c.hits.p, seed_term, (int)last, ctr.p);                                               \
+                           c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p, seed_term,   \
+                           (int)last, ctr.p);                                                                    \
     } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
     do {                                                                                                         \
@@ -1054,10 +1057,11 @@ struct rt_renderer {
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(e1, st));
             if (!sort && b + 1 != bounces) {
-                hipLaunchKernelGGL(compact_live_kernel, dim3(sgrid), dim3(kBlock), 0, st, b == 0 ? nullptr : c.list[lcur].p,
-                                   c.bkt.p, lv, c.list[1 - lcur].p, c.live.p + b + 1);
+                hipLaunchKernelGGL(compact_live_kernel, dim3(sgrid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                   c.tc[cur].p, c.rid[cur].p, lv, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p,
+                                   c.live.p + b + 1, (int)(b == 0));
                 HIPCHK(hipGetLastError());
-                lcur = 1 - lcur;
+                cur = 1 - cur;
             }
             if (sort && b + 1 != bounces) {
                 hipEvent_t s0 = c.event(), s1 = c.event();
@@ -1086,7 +1090,7 @@ struct rt_renderer {
             HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
         } else {
             hipLaunchKernelGGL(accumulate_kernel, dim3((unsigned)((pixels + kAccPixels - 1) / kAccPixels)), dim3(kBlock),
-                               0, st, sort ? c.acc.p : c.tc[0].p, rtc, (int)pixels, sums);
+                               0, st, c.acc.p, rtc, (int)pixels, sums);
         }
         HIPCHK(hipGetLastError());
         return RT_OK;
@@ -1121,10 +1125,10 @@ struct rt_renderer {
         const int tgrid = std::min(blocks_for(n), trace_blocks);
         if (counters)
             hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               nullptr, live.p, queue.p, hits.p, overflow.p, ctr.p);
+                               live.p, queue.p, hits.p, overflow.p, ctr.p);
         else
             hipLaunchKernelGGL((trace_kernel<false, false, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               nullptr, live.p, queue.p, hits.p, overflow.p, ctr.p);
+                               live.p, queue.p, hits.p, overflow.p, ctr.p);
         HIPCHK(hipGetLastError());
         std::vector<float2> h((size_t)n);
         HIPCHK(hipMemcpyAsync(h.data(), hits.p, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, s0));
