@@ -507,52 +507,12 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
     }
 }
 
-// live[0] = n; the later counts are n (sort on: the reorder's scan overwrites them) or 0 (sort
-// off: the live-list compaction counts into them).
-__global__ void fill_live_kernel(uint32_t *__restrict__ live, uint32_t n, int count, uint32_t later,
-                                 uint32_t *__restrict__ queue) {
+__global__ void fill_live_kernel(uint32_t *__restrict__ live, uint32_t n, int count, uint32_t *__restrict__ queue) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < count) live[i] = i == 0 ? n : later;
+    if (i < count) live[i] = n;
     for (int k = i; k < count * kQueues * kQueueStride; k += blockDim.x) queue[k] = 0;
 }
 
-
-// Sort off: the rays still live after a bounce move (with their state, like the reorder's
-// scatter) to the front of the next buffers, so the next bounce visits only them, in slot
-// order.  Their order there is irrelevant: a ray keeps its seed slot (its ray id) and its
-// state, so a wave appends its live rays with one atomic.
-__global__ __launch_bounds__(kBlock) void compact_live_kernel(const uint8_t *__restrict__ bkt,
-                                                              const float4 *__restrict__ geo_in,
-                                                              const float4 *__restrict__ tc_in,
-                                                              const uint32_t *__restrict__ rid_in,
-                                                              const uint32_t *__restrict__ live_count,
-                                                              float4 *__restrict__ geo_out, float4 *__restrict__ tc_out,
-                                                              uint32_t *__restrict__ rid_out,
-                                                              uint32_t *__restrict__ live_next, int first) {
-    const uint32_t L = *live_count;
-    for (uint32_t base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
-        const uint32_t k = base + threadIdx.x;
-        const bool alive = k < L && bkt[k] != kDead;
-        float4 g0 = make_float4(0, 0, 0, 0), g1 = g0, t = g0;
-        uint32_t id = 0;
-        if (alive) {
-            g0 = geo_in[(size_t)k * 2];
-            g1 = geo_in[(size_t)k * 2 + 1];
-            t = tc_in[k];
-            id = first ? k : rid_in[k];
-        }
-        const unsigned long long m = __ballot(alive);
-        uint32_t at = 0;
-        if (lane_id() == 0 && m) at = atomicAdd(live_next, (uint32_t)__popcll(m));
-        at = __shfl(at, 0) + rank_below(m);
-        if (alive) {
-            geo_out[(size_t)at * 2] = g0;
-            geo_out[(size_t)at * 2 + 1] = g1;
-            tc_out[at] = t;
-            rid_out[at] = id;
-        }
-    }
-}
 
 // ---------------------------------------------------------------- stable 65-bucket reorder
 // Equivalent to cub::DeviceRadixSort::SortPairs on the reference keys (raytracing.cu:238-247).
@@ -974,11 +934,9 @@ struct rt_renderer {
             }
             if ((rc = c.bkt.alloc((size_t)max_rays))) return rc;
             if ((rc = c.acc.alloc((size_t)max_rays))) return rc;
-            if (sort) {
-                if ((rc = c.sort_counts.alloc((size_t)kBuckets * tiles))) return rc;
-                if ((rc = c.sort_offsets.alloc((size_t)kBuckets * tiles))) return rc;
-                if ((rc = c.sort_totals.alloc(kBuckets))) return rc;
-            }
+            if ((rc = c.sort_counts.alloc((size_t)kBuckets * tiles))) return rc;
+            if ((rc = c.sort_offsets.alloc((size_t)kBuckets * tiles))) return rc;
+            if ((rc = c.sort_totals.alloc(kBuckets))) return rc;
             if ((rc = c.live.alloc((size_t)bounces + 1))) return rc;
             if ((rc = c.queue.alloc((size_t)(bounces + 1) * kQueues * kQueueStride))) return rc;
             if ((rc = c.hits.alloc((size_t)max_rays))) return rc;
@@ -1024,8 +982,7 @@ struct rt_renderer {
         const int sgrid = std::min(grid, cus * 8);
         hipStream_t st = c.stream;
         int cur = 0;
-        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1,
-                           sort ? (uint32_t)n : 0u, c.queue.p);
+        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1, c.queue.p);
         const PassArgs pa{rtc, 709579u * (uint32_t)remaining, FastDiv::of((uint32_t)rtc), FastDiv::of((uint32_t)width)};
         for (int b = 0; b < bounces; b++) {
             const uint32_t seed_term = 279220567u * (uint32_t)(remaining * 20 + b);
@@ -1056,14 +1013,9 @@ struct rt_renderer {
 #undef RT_PROCESS3
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(e1, st));
-            if (!sort && b + 1 != bounces) {
-                hipLaunchKernelGGL(compact_live_kernel, dim3(sgrid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                   c.tc[cur].p, c.rid[cur].p, lv, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p,
-                                   c.live.p + b + 1, (int)(b == 0));
-                HIPCHK(hipGetLastError());
-                cur = 1 - cur;
-            }
-            if (sort && b + 1 != bounces) {
+            // The reorder (sort off: every live ray has bucket 0, so it is a stable compaction
+            // of the live rays) moves the live rays' state for the next bounce.
+            if (b + 1 != bounces) {
                 hipEvent_t s0 = c.event(), s1 = c.event();
                 if (!s0 || !s1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
                 HIPCHK(hipEventRecord(s0, st));
@@ -1082,7 +1034,7 @@ struct rt_renderer {
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventRecord(s1, st));
                 cur = 1 - cur;
-                sorted += n;
+                if (sort) sorted += n;
             }
         }
         if (bounces == 0) {
