@@ -5,9 +5,10 @@ Workload (default): teapot.scene at 1920x1080, 2048 spp, 16 bounces, sort on (BA
 configs[3], the config the north star's roofline target is stated on).  A step is one 20-spp
 pass of the hot path on every GPU: ray generation, 16 x (BVH traversal + shading + reorder
 key, stable reorder), ordered accumulation.  Multi-GPU runs shard whole passes round-robin
-over ranks (rank r renders pass r + N*k); each step ends with an RCCL gather of the per-pass
-framebuffers to rank 0, which adds them in pass order (bit-identical to 1 GPU).  Per-GPU work
-is fixed, so scaling is weak.
+over ranks (rank r renders pass r + N*k); the pass framebuffers are exchanged as pixel slices
+(one RCCL all-to-all: rank j owns slice j and adds the slices in pass order, bit-identical to
+1 GPU) and the finished slices are gathered to rank 0.  By default the timed region is one
+full frame (strong scaling); `--steps K` times K passes per GPU (weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scene teapot] [--no-sort]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -25,7 +26,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-# The renderer keeps up to 12 passes in flight on their own streams; with torch/RCCL streams in the
+# The renderer keeps up to 16 passes in flight on their own streams; with torch/RCCL streams in the
 # same process HIP's default of 4 hardware queues would make them share queues.  Set before HIP
 # initialises.
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
@@ -111,6 +112,11 @@ def main():
     ap.add_argument("--no-counters", action="store_true", help="skip the byte-model counting rerun")
     ap.add_argument("--dist", action="store_true", help="use the torch.distributed path even at N=1")
     args = ap.parse_args()
+    # The JSON line is the only thing on stdout: native libraries (RCCL prints a version banner)
+    # write to stdout too, so fd 1 is pointed at stderr and the line goes to a saved copy of it.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -160,8 +166,7 @@ def main():
     steps = R if full_frame else args.steps
     if use_dist:
         import rtamd_dist
-        frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, torch.device("cuda", local), render_passes,
-                                            max_rounds_per_call=32)
+        frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, torch.device("cuda", local), render_passes)
 
     def barrier_sync():
         if use_dist:
@@ -176,9 +181,12 @@ def main():
         while done < k:
             m = min(k - done, R)
             if use_dist:
-                # this rank's passes of those rounds, then per round an RCCL gather of the pass
-                # framebuffers to rank 0, which adds them in pass order (rtamd_dist.PassShardedFrame)
+                # this rank's passes of those rounds in one renderer call, then one RCCL all-to-all
+                # of pixel slices to their owners, which add them in pass order, and a gather of the
+                # finished slices to rank 0 (rtamd_dist.PassShardedFrame)
+                frame.reset()
                 mine += frame.run_rounds(0, m)
+                frame.collect()
             else:
                 accumulate_stats(ren.run(pass_begin=0, count=m, stride=1))
                 mine += m
@@ -228,7 +236,7 @@ def main():
         roof = None
         if counted:
             bytes_launch = bytes_total / launches
-            # Up to 12 passes are in flight, so process launches of different passes overlap and a
+            # Up to 16 passes are in flight, so process launches of different passes overlap and a
             # launch's own duration overstates its share of the GPU: `achieved` is the process
             # kernels' algorithmic bytes over the wall time of the timed steps (conservative: the
             # wall also covers reorder/accumulate); the per-launch figure is reported too.
@@ -276,7 +284,7 @@ def main():
                 "workload": workload,
                 "step": "one 20-spp pass (%d rays x %d bounces) per GPU; pass-sharded over GPUs" % (20 * W * H, bounces),
                 "timed": ("one full frame (%d passes)" % P) if full_frame else ("%d passes per GPU" % steps),
-                "parallelism": "pass-shard x%d + RCCL gather" % world if world > 1 else "single GPU",
+                "parallelism": "pass-shard x%d + RCCL all-to-all/gather" % world if world > 1 else "single GPU",
                 "nominal_mrays_per_s": round(nominal, 2),
                 "render_wall_ms": round(elapsed * 1e3, 1) if full_frame else None,
                 "render_wall_ms_projected": round(ms_step * R, 1),
@@ -297,7 +305,7 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(cfg, args)
             except Exception as e:  # reported, never fatal for the GPU numbers
                 out["cpu_baseline"] = {"error": str(e)}
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     ren.close()
     if use_dist:
         dist.barrier()

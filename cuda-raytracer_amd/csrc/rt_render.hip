@@ -48,7 +48,7 @@ namespace {
 #define RT_CHUNK_MAX 128
 #endif
 #ifndef RT_INFLIGHT
-#define RT_INFLIGHT 12
+#define RT_INFLIGHT 16
 #endif
 #ifndef RT_TRACE_OCC
 #define RT_TRACE_OCC 40

@@ -4,10 +4,14 @@ The render is a sequence of independent 20-spp passes (raytracing.cu:222-254): e
 its own generate seed (`remaining`), its own per-bounce process seeds and its own stable
 reorder, so a pass renders identically on any GPU.  Rank r renders passes r, r+N, r+2N, ...
 (round-robin keeps the load balanced: passes cost the same, except a shorter last pass).
-After every round of N passes the per-pass framebuffers are gathered to rank 0, which adds them
-in pass order: fb = ((0 + S_0) + S_1) + ... exactly as one GPU does, so the N-GPU image is
-bit-identical to the 1-GPU image.  This is the only exchange (24.9 MB per pass at 1080p);
-there is no per-bounce collective.
+
+Accumulation is owned per pixel slice: the framebuffer (W*H*3 floats) is cut into N equal
+slices and rank j owns slice j.  After a chunk of rounds every rank sends slice j of each of
+its pass framebuffers to rank j in one all-to-all (RCCL over xGMI: every link carries 1/N of
+the data, nothing converges on one GPU), and each owner adds the pass slices it received in
+pass order: fb_j = ((0 + S_0,j) + S_1,j) + ... exactly as one GPU adds whole passes, so the
+N-GPU image is bit-identical to the 1-GPU image.  `collect()` gathers the N finished slices to
+rank 0 (one framebuffer, 24.9 MB at 1080p).  There is no per-bounce collective.
 """
 from typing import Callable, List, Optional
 
@@ -21,53 +25,86 @@ def rounds(world: int, passes: int) -> int:
     return -(-passes // world)
 
 
+def slice_len(pixels3: int, world: int) -> int:
+    """Floats per owner slice (the last slice is padded)."""
+    return -(-pixels3 // world)
+
+
 class PassShardedFrame:
     """Accumulates a frame rendered pass-sharded over the ranks of a process group.
 
     render_passes(passes, out) must write pass passes[j]'s per-pixel sum (W*H*3 float32) into
     out[j], a 2-D tensor on `device`; handing several passes to one call lets the renderer keep
-    several passes in flight.  Rank 0 owns the accumulated framebuffer `fb`.
+    several passes in flight (the default chunk is the whole frame, one call per rank).
+    After `collect()`, rank 0 holds the accumulated framebuffer in `fb`.
     """
 
     def __init__(self, dist, torch, pixels3: int, passes: int, device, render_passes: Callable,
-                 max_rounds_per_call: int = 8):
+                 max_rounds_per_call: Optional[int] = None):
         self.dist, self.torch = dist, torch
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
+        self.pixels3 = pixels3
         self.passes = passes
         self.render_passes = render_passes
-        self.chunk = max_rounds_per_call
+        self.chunk = max(1, min(max_rounds_per_call or rounds(self.world, passes), rounds(self.world, passes)))
+        self.sl = slice_len(pixels3, self.world)
         f32 = torch.float32
-        self.buf = torch.zeros((self.chunk, pixels3), dtype=f32, device=device)
-        self.gather = [torch.zeros(pixels3, dtype=f32, device=device) for _ in range(self.world)] \
-            if self.rank == 0 else None
-        self.fb: Optional[object] = torch.zeros(pixels3, dtype=f32, device=device) if self.rank == 0 else None
+        # pass framebuffers, row stride padded to N slices so a row splits into N equal pieces
+        self.buf = torch.zeros((self.chunk, self.world * self.sl), dtype=f32, device=device)
+        self.slice = torch.zeros(self.sl, dtype=f32, device=device)   # this rank's owned slice
+        # the renderer writes contiguous W*H*3 rows; when N does not divide that, it renders into
+        # a staging buffer that is copied into the padded rows
+        self.stage = None if self.world * self.sl == pixels3 else \
+            torch.zeros((self.chunk, pixels3), dtype=f32, device=device)
+        self.fb: Optional[object] = None
+
+    def reset(self):
+        self.slice.zero_()
+        self.fb = None
 
     def run_rounds(self, k0: int, nrounds: int) -> int:
         """Rounds k0 .. k0+nrounds-1: rank r renders passes r + N*k (those that exist) in one
-        renderer call per chunk, then each round is gathered to rank 0 and added in pass order.
-        Returns the number of passes this rank rendered."""
+        renderer call per chunk; the pass slices go to their owners, which add them in pass
+        order.  Returns the number of passes this rank rendered."""
         done = 0
+        N, sl = self.world, self.sl
         for c0 in range(k0, k0 + nrounds, self.chunk):
             ks = list(range(c0, min(c0 + self.chunk, k0 + nrounds)))
-            mine = [self.rank + self.world * k for k in ks if self.rank + self.world * k < self.passes]
+            m = len(ks)
+            mine = [self.rank + N * k for k in ks if self.rank + N * k < self.passes]
             if mine:
-                self.render_passes(mine, self.buf[:len(mine)])
+                if self.stage is None:
+                    self.render_passes(mine, self.buf[:len(mine)])
+                else:
+                    self.render_passes(mine, self.stage[:len(mine)])
+                    self.buf[:len(mine), :self.pixels3].copy_(self.stage[:len(mine)])
+            if N > 1:
+                # send[d, j] = slice d of this rank's pass framebuffer of round ks[j]
+                send = self.buf[:m].view(m, N, sl).transpose(0, 1).contiguous()
+                recv = self.torch.empty_like(send)
+                self.dist.all_to_all_single(recv, send)
+            else:
+                recv = self.buf[:m].view(1, m, sl)
             for j, k in enumerate(ks):
-                src = self.buf[j] if j < len(mine) else self.buf[-1].zero_()
-                if self.world > 1:
-                    self.dist.gather(src, gather_list=self.gather, dst=0)
-                elif self.rank == 0:
-                    self.gather = [src]
-                if self.rank == 0:
-                    for r in range(self.world):
-                        if r + self.world * k < self.passes:
-                            self.fb.add_(self.gather[r])
+                for src in range(N):            # pass src + N*k: ascending pass order
+                    if src + N * k < self.passes:
+                        self.slice.add_(recv[src, j])
             done += len(mine)
         return done
 
-    def run_round(self, k: int) -> int:
-        return self.run_rounds(k, 1)
+    def collect(self):
+        """Gathers the owned slices to rank 0 (collective); returns rank 0's framebuffer."""
+        if self.world > 1:
+            parts = [self.torch.empty_like(self.slice) for _ in range(self.world)] if self.rank == 0 else None
+            self.dist.gather(self.slice, gather_list=parts, dst=0)
+            if self.rank == 0:
+                self.fb = self.torch.cat(parts)[:self.pixels3]
+        else:
+            self.fb = self.slice[:self.pixels3]
+        return self.fb
 
     def run_all(self) -> int:
-        return self.run_rounds(0, rounds(self.world, self.passes))
+        n = self.run_rounds(0, rounds(self.world, self.passes))
+        self.collect()
+        return n

@@ -1,7 +1,8 @@
-"""N>1 path on CPU: world_size-2 gloo process group running the same pass-sharding and ordered
-gather code (rtamd_dist.PassShardedFrame) that bench.py runs over RCCL.  Pass sums come from the
-oracle here (the GPU renders them on the box); the assembled frame must be bit-identical to
-the single-process render."""
+"""N>1 path on CPU: gloo process groups (world 2, 3, 5) running the same pass-sharding,
+pixel-slice all-to-all and ordered per-slice accumulation (rtamd_dist.PassShardedFrame) that
+bench.py runs over RCCL.  Pass sums come from the oracle here (the GPU renders them on the box);
+the assembled frame must be bit-identical to the single-process render.  World 5 does not divide
+W*H*3 = 1152, so it covers the padded-slice path; chunk 2 covers several exchanges per frame."""
 import os
 import socket
 
@@ -25,7 +26,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, chunk):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sc = O.OracleScene(os.path.join(O.ASSETS, "cornell_plus.scene"), image=IMAGE)
@@ -34,7 +35,7 @@ def _worker(rank, world, port, out_path):
         for j, p in enumerate(passes):
             out[j].copy_(torch.from_numpy(sc.pass_sums(sort=True, pass_begin=p, pass_count=1, threads=2)[0]))
 
-    frame = D.PassShardedFrame(dist, torch, sc.pixels * 3, sc.passes, "cpu", render_passes, max_rounds_per_call=2)
+    frame = D.PassShardedFrame(dist, torch, sc.pixels * 3, sc.passes, "cpu", render_passes, max_rounds_per_call=chunk)
     n = frame.run_all()
     assert n == len(D.pass_schedule(rank, world, sc.passes))
     if rank == 0:
@@ -42,10 +43,10 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_pass_sharded_frame_is_bitexact(tmp_path, world):
+@pytest.mark.parametrize("world,chunk", [(2, 2), (3, None), (5, None)])
+def test_pass_sharded_frame_is_bitexact(tmp_path, world, chunk):
     out = str(tmp_path / "fb.npy")
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, chunk), nprocs=world, join=True)
     got = np.load(out)
     ref, _ = O.OracleScene(os.path.join(O.ASSETS, "cornell_plus.scene"), image=IMAGE).render(sort=True)
     assert np.array_equal(got, ref)
