@@ -42,7 +42,7 @@ namespace {
 #define RT_REFILL 16
 #endif
 #ifndef RT_REFILL_FIRST
-#define RT_REFILL_FIRST 16
+#define RT_REFILL_FIRST 64
 #endif
 #ifndef RT_CHUNK_MAX
 #define RT_CHUNK_MAX 128
@@ -66,7 +66,8 @@ constexpr int kCtrSlots = 64;       // striped copies of the work counters
 constexpr int kChunkMax = RT_CHUNK_MAX; // slots a wave takes from the trace queue per atomic...
 constexpr int kChunkMin = 64;        // ...shrunk so that every wave gets ~4 chunks when few rays live
 constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are idle
-constexpr int kRefillFirst = RT_REFILL_FIRST;   // same at bounce 0 (primary-ray setup is dearer)
+constexpr int kRefillFirst = RT_REFILL_FIRST;   // same at bounce 0: a whole wave of consecutive primary rays
+                                                // (~3 pixels) starts together and stays in lockstep
 constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffer set each)
 constexpr int kTraceOccPct = RT_TRACE_OCC; // % of the resident trace workgroups the persistent grid uses
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
@@ -90,7 +91,7 @@ struct DevScene {
 
 #ifdef RT_PROFILE
 // Wave-level traversal profile (debug builds only): see tools/variants.sh + RT_PROFILE=1.
-__device__ unsigned long long g_prof[8];
+__device__ unsigned long long g_prof[2][12];   // [bounce 0, later bounces]
 #define PROF(i, v) (prof[i] += (v))
 #else
 #define PROF(i, v) ((void)0)
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     int ti = 0, te = 0;                 // the lane is in a leaf while ti < te
     unsigned pn = 0, iv = 0, tt = 0, nlive = 0;
 #ifdef RT_PROFILE
-    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long prof[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     while (true) {
         // ---- refill idle lanes (wave-uniform control flow)
@@ -309,6 +310,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             const unsigned long long act = __ballot(slot >= 0), lf = __ballot(slot >= 0 && ti < te);
             PROF(0, 1); PROF(1, __popcll(act)); PROF(2, __popcll(lf));
             PROF(3, lf != 0); PROF(4, (act & ~lf) != 0);
+            const bool mixed = lf != 0 && (act & ~lf) != 0;
+            PROF(8, mixed);
+            if (mixed) PROF(9, min(__popcll(lf), __popcll(act & ~lf)));
         }
 #endif
         if (slot < 0) continue;
@@ -380,6 +384,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         if (__ballot(need)) PROF(5, 1);
 #endif
         while (need) {                  // pop to the next entry nearer than closest
+            PROF(10, 1);
             if (sp == 0) {
                 hits[slot] = make_float2(closest, __int_as_float(index));
                 slot = -1;
@@ -419,8 +424,10 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     }
     if (lane_id() == 0 && nl) atomicAdd(&cs->live, nl);
 #ifdef RT_PROFILE
+    prof[11] = wave_sum((unsigned)prof[10]);   // pop iterations summed over the lanes
     if (lane_id() == 0)
-        for (int i = 0; i < 8; i++) atomicAdd(&g_prof[i], prof[i]);
+        for (int i = 0; i < 12; i++)
+            if (i != 10) atomicAdd(&g_prof[FIRST ? 0 : 1][i], prof[i]);
 #endif
 }
 
@@ -1141,12 +1148,17 @@ struct rt_renderer {
         HIPCHK(hipStreamSynchronize(s0));
 #ifdef RT_PROFILE
         {
-            unsigned long long pr[8];
+            unsigned long long pr[2][12];
             HIPCHK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof(pr)));
-            const double it = (double)pr[0];
-            std::fprintf(stderr, "RT_PROFILE wave_iters %llu active/iter %.2f leaf/iter %.2f iters_with_leaf %.3f "
-                         "iters_with_inner %.3f iters_with_pop %.3f refills/iter %.3f idle_iters %llu\n",
-                         pr[0], pr[1] / it, pr[2] / it, pr[3] / it, pr[4] / it, pr[5] / it, pr[6] / it, pr[7]);
+            for (int f = 0; f < 2; f++) {
+                const unsigned long long *q = pr[f];
+                const double it = (double)std::max(1ull, q[0]);
+                std::fprintf(stderr, "RT_PROFILE %s wave_iters %llu active/iter %.2f leaf/iter %.2f iters_with_leaf %.3f "
+                             "iters_with_inner %.3f iters_with_pop %.3f refills/iter %.3f idle_iters %llu mixed %.3f "
+                             "minority/mixed %.2f lane_pops/iter %.3f\n",
+                             f ? "later" : "bounce0", q[0], q[1] / it, q[2] / it, q[3] / it, q[4] / it, q[5] / it,
+                             q[6] / it, q[7], q[8] / it, q[9] / (double)std::max(1ull, q[8]), q[11] / it);
+            }
             std::memset(pr, 0, sizeof(pr));
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));
         }
