@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 step() { echo "== $*"; }
 step tests
-timeout -k 10 500 python -m pytest tests -m gpu -q > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
 tail -1 $OUT/gpu_tests.log
 step bench teapot
 timeout -k 10 400 python bench.py > $OUT/bench_teapot.json 2> $OUT/bench_teapot.err || { tail $OUT/bench_teapot.err; exit 1; }
@@ -21,4 +21,8 @@ step rocprof kernel trace
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-counters > $OUT/prof.log 2>&1 || { tail $OUT/prof.log; exit 1; }
 step pmc traffic
 bash tools/pmc.sh ${TAG}_tf tools/pmc_groups/traffic.txt || exit 1
+step pmc trace
+bash tools/pmc.sh ${TAG}_tr tools/pmc_groups/trace.txt || exit 1
+step strong-scaling probe
+bash tools/scaling_probe.sh $TAG/scaling || exit 1
 echo done
