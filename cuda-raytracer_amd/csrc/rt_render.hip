@@ -197,11 +197,12 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 // chunks of slots from a device queue (one atomic per chunk) and hands a new slot to a lane
 // as soon as that lane's ray is done, so incoherent rays of very different traversal lengths
 // do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
-#ifdef RT_TRACE_WPE
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, 8)))
-#else
-#define RT_TRACE_ATTR
+// 8 waves per SIMD (<= 64 VGPRs): the one spill left is a lane constant reloaded only on the
+// overflow-stack path.  +2 % over the unconstrained 66 VGPRs (7 waves).
+#ifndef RT_TRACE_WPE
+#define RT_TRACE_WPE 8
 #endif
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, 8)))
 template <bool SORTED, bool COUNT, bool FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ live_count,
@@ -210,12 +211,12 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
     uint2 *col = stack + threadIdx.x;
     // Overflow tail of the stack (entries >= kStackLds, rare) in a global per-lane buffer,
-    // [entry][lane] for coalescing; stored as two 32-bit arrays so the compiler cannot fuse the
-    // LDS and global pops into one flat load.
-    const size_t lanes = (size_t)gridDim.x * kBlock;
-    uint32_t *ovf_ref = overflow + (size_t)blockIdx.x * kBlock + threadIdx.x;
-    float *ovf_dist = reinterpret_cast<float *>(overflow + lanes * (kStackMax - kStackLds)) +
-                      (size_t)blockIdx.x * kBlock + threadIdx.x;
+    // [entry][lane] for coalescing; refs and distances in two 32-bit halves so the compiler cannot
+    // fuse the LDS and global pops into one flat load.
+    // Entry e >= kStackLds of this lane's overflow: ref at overflow[e' * lanes + lane], dist in the
+    // second half (e' = e - kStackLds), addressed on use (the path is rare; no pointer registers).
+    const uint32_t lanes = gridDim.x * kBlock, gl = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t dist_half = lanes * (kStackMax - kStackLds);
     const uint32_t L = __builtin_amdgcn_readfirstlane(*live_count);
     const uint32_t waves = gridDim.x * (kBlock / 64);
     const uint32_t chunk = min((uint32_t)kChunkMax, max((uint32_t)kChunkMin, (L / (4 * waves) + 63) & ~63u));
@@ -365,8 +366,8 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             // kStackLds is a scratch slot), so the push needs no branch
             col[min(sp, kStackLds) * kBlock] = make_uint2(near_ref, __float_as_uint(near_t));
             if (__builtin_expect(both & (sp >= kStackLds), 0)) {
-                ovf_ref[(sp - kStackLds) * lanes] = near_ref;
-                ovf_dist[(sp - kStackLds) * lanes] = near_t;
+                overflow[(sp - kStackLds) * lanes + gl] = near_ref;
+                overflow[dist_half + (sp - kStackLds) * lanes + gl] = __float_as_uint(near_t);
             }
             sp += both ? 1 : 0;
             ref = any ? next_ref : ref;
@@ -398,8 +399,8 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 eref = e.x;
                 edist = __uint_as_float(e.y);
             } else {
-                eref = ovf_ref[(sp - kStackLds) * lanes];
-                edist = ovf_dist[(sp - kStackLds) * lanes];
+                eref = overflow[(sp - kStackLds) * lanes + gl];
+                edist = __uint_as_float(overflow[dist_half + (sp - kStackLds) * lanes + gl]);
             }
             if (edist >= closest) continue;
             ref = eref;

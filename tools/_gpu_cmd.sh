@@ -1,7 +1,3 @@
 export TMPDIR=/tmp
-for q in 16 24 32; do
-  for m in "--dist" ""; do
-    GPU_MAX_HW_QUEUES=$q timeout -k 10 200 python bench.py --no-counters --no-cpu-baseline $m > gpurun_out/q.json 2> gpurun_out/q.err || { tail gpurun_out/q.err; exit 1; }
-    python3 -c "import json;d=json.load(open('gpurun_out/q.json'));print('queues $q', '$m', d['ms_per_step'])"
-  done
-done
+RTAMD_LIB=cuda-raytracer_amd/build_var/wpe8/librtamd.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_edge_scenes.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t6.log 2>&1; tail -1 gpurun_out/t6.log
+timeout -k 10 900 python tools/ab.py 3 default wpe8 wpe8o35 wpe8o50 -- --steps 40 > gpurun_out/ab_wpe.log 2>&1; tail -5 gpurun_out/ab_wpe.log
