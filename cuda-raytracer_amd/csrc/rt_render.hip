@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -777,6 +778,22 @@ bool is_leaf(const rt_bvh_node &nd) { return nd.child2 <= nd.child1; }   // scen
 }  // namespace
 
 // Device state of one in-flight pass: its own stream, ray state, reorder buffers and queues.
+// Phase timing of renderer setup, printed to stderr when RTAMD_TIMING is set.
+struct InitTimer {
+    std::chrono::high_resolution_clock::time_point t = std::chrono::high_resolution_clock::now();
+    std::string out;
+    bool on = std::getenv("RTAMD_TIMING") != nullptr;
+    void mark(const char *what) {
+        if (!on) return;
+        const auto now = std::chrono::high_resolution_clock::now();
+        char buf[96];
+        std::snprintf(buf, sizeof(buf), " %s %.1f ms,", what, std::chrono::duration<double, std::milli>(now - t).count());
+        out += buf;
+        t = now;
+    }
+    void report() const { if (on) std::fprintf(stderr, "rt_renderer init:%s\n", out.c_str()); }
+};
+
 struct PassCtx {
     hipStream_t stream = nullptr;
     // Ray state in slot order, ping-ponged by the reorder (sort off: one copy, slot = ray id):
@@ -797,6 +814,13 @@ struct PassCtx {
         if (fb_done) (void)hipEventDestroy(fb_done);
         if (done) (void)hipEventDestroy(done);
         if (stream) (void)hipStreamDestroy(stream);
+    }
+    int open() {
+        if (stream) return RT_OK;
+        HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&fb_done, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        return RT_OK;
     }
     hipEvent_t event() {
         if (ev == events.size()) {
@@ -841,12 +865,13 @@ struct rt_renderer {
         height = sc->height;
         spp = sc->ray_count;
         bounces = sc->bounces;
+        InitTimer tm;
         HIPCHK(hipSetDevice(device));
-        for (auto &c : ctx) {
-            HIPCHK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&c.fb_done, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
-        }
+        tm.mark("hipSetDevice");
+        // streams cost ~3.6 ms each to create and ~2 ms to destroy: context 0's now, the other
+        // contexts' once the number of passes in flight is known
+        if (int rc0 = ctx[0].open()) return rc0;
+        tm.mark("first stream");
         HIPCHK(hipEventCreate(&t_begin));
         HIPCHK(hipEventCreate(&t_end));
         hipStream_t s0 = stream();
@@ -921,7 +946,9 @@ struct rt_renderer {
         if ((rc = ctr.alloc(kCtrSlots))) return rc;
         int per_cu = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        tm.mark("scene upload");
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<true, false, false>, kBlock, 0));
+        tm.mark("occupancy query");
         trace_blocks = std::max(1, cus * std::max(1, per_cu) * kTraceOccPct / 100);
         const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
@@ -935,6 +962,7 @@ struct rt_renderer {
         const int inflight = nctx;
         for (int k = 0; k < inflight; k++) {
             PassCtx &c = ctx[k];
+            if ((rc = c.open())) return rc;
             for (int q = 0; q < 2; q++) {
                 if ((rc = c.geo[q].alloc((size_t)max_rays * 2))) return rc;
                 if ((rc = c.tc[q].alloc((size_t)max_rays))) return rc;
@@ -951,6 +979,7 @@ struct rt_renderer {
             if ((rc = c.overflow.alloc((size_t)trace_blocks * kBlock * 2 * (kStackMax - kStackLds)))) return rc;
             if ((rc = c.psum.alloc((size_t)pixels * 3))) return rc;
         }
+        tm.mark("pass contexts");
         HIPCHK(hipMemsetAsync(fb.p, 0, fb.n * sizeof(float), s0));
         ds.spheres = spheres.p;
         ds.tris = tris.p;
@@ -973,6 +1002,8 @@ struct rt_renderer {
         ds.inv_w = sc->inv_width;
         ds.inv_h = sc->inv_height;
         HIPCHK(hipStreamSynchronize(s0));
+        tm.mark("sync");
+        tm.report();
         return RT_OK;
     }
 
@@ -1265,6 +1296,22 @@ int rt_device_count(void) {
     return n;
 }
 
+int rt_device_warmup(int32_t device) {
+    if (device < 0 || device >= rt_device_count()) return rtamd::fail(RT_E_NODEVICE, "no such HIP device");
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    uint32_t *d = nullptr;
+    HIPCHK(hipMallocAsync(reinterpret_cast<void **>(&d), 4 * sizeof(uint32_t), s));
+    // one (empty: count 0 writes nothing) launch loads this library's code object on the device
+    hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, s, d, 0u, 0, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipFreeAsync(d, s));
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipStreamDestroy(s));
+    return RT_OK;
+}
+
 int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer **out) {
     if (!out) return rtamd::fail(RT_E_INVALID, "null output");
     *out = nullptr;
@@ -1327,18 +1374,30 @@ int rt_renderer_set_counters(rt_renderer *r, int32_t enable) {
 void rt_renderer_destroy(rt_renderer *r) { delete r; }
 
 int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stats *stats) {
-    const auto w0 = std::chrono::high_resolution_clock::now();
+    using clk = std::chrono::high_resolution_clock;
+    const auto w0 = clk::now();
+    auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
     if (!fb_out) return rtamd::fail(RT_E_INVALID, "null framebuffer");
     rt_opts o;
     if (opts) o = *opts; else rt_default_opts(&o);
     rt_renderer *r = nullptr;
     int rc = rt_renderer_create(scene, &o, &r);
     if (rc) return rc;
+    const double t_create = ms_since(w0);
+    auto w1 = clk::now();
     rc = r->run(o.pass_begin, o.pass_count, o.pass_stride, nullptr, stats);
+    const double t_run = ms_since(w1);
+    w1 = clk::now();
     if (!rc) rc = rt_renderer_read_framebuffer(r, fb_out);
+    const double t_read = ms_since(w1);
+    w1 = clk::now();
+    const int inflight = r->nctx;
     delete r;
-    if (!rc && stats)
-        stats->render_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
+    const double t_free = ms_since(w1);
+    if (std::getenv("RTAMD_TIMING"))
+        std::fprintf(stderr, "rt_render: create %.1f ms (%d passes in flight), run %.1f ms, read %.1f ms, destroy %.1f ms\n",
+                     t_create, inflight, t_run, t_read, t_free);
+    if (!rc && stats) stats->render_ms = ms_since(w0);
     return rc;
 }
 

@@ -125,6 +125,11 @@ def _ptr(a):
     return a.ctypes.data_as(P)
 
 
+def warmup(device=0):
+    """rt_device_warmup: HIP runtime, queues and code object initialised on `device`."""
+    _check(lib().rt_device_warmup(device))
+
+
 def device_count():
     return lib().rt_device_count()
 

@@ -121,6 +121,11 @@ typedef struct {
 void rt_default_opts(rt_opts *opts);
 void rt_default_load_opts(rt_load_opts *opts);
 int rt_device_count(void);
+/* Initialises the HIP runtime, the device's queues and the kernel code object on `device`
+ * (what the first render would otherwise pay, ~0.2 s per process).  Thread-safe; a host can call
+ * it on a thread of its own while it loads the scene, as the CLI does.  No reference
+ * counterpart: the reference pays CUDA context creation inside gpu_raytrace (raytracing.cu:174). */
+int rt_device_warmup(int32_t device);
 
 /* Replaces `Vec3 *gpu_raytrace(const Scene *scene, bool sort)` (raytracing.cu:170-284):
  * uploads the scene, renders every pass selected by opts, and writes the accumulated

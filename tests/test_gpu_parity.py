@@ -83,6 +83,13 @@ def test_pass_sharding_matches_full_render(gpu):
     assert np.array_equal(odd, (np.zeros_like(full) + sums[1]))
 
 
+def test_device_warmup(gpu):
+    R.warmup(0)
+    R.warmup(0)                       # idempotent
+    with pytest.raises(R.RtError):
+        R.warmup(R.device_count())    # no such device
+
+
 def test_bloom_bitexact(gpu):
     rng = np.random.default_rng(7)
     w, h = 97, 61
