@@ -2,7 +2,7 @@
 //
 //   raytracing <scene file> [no_sort] [cpu] [no_gpu] [no_bvh]
 //              [--image W H spp bounces exposure] [--devices N] [--device K]
-//              [--asset-root DIR] [--out FILE] [--stats FILE]
+//              [--asset-root DIR] [--out FILE] [--stats FILE] [--gpu-bvh]
 //
 // Reference behaviour kept: usage line + exit 1 without a scene, "No raytracing hardware
 // specified" + exit 2 for no_gpu without cpu, unknown words ignored, asset paths relative to
@@ -87,7 +87,7 @@ int main(int argc, char **argv) {
         std::printf("Usage: %s <scene>\n", argv[0]);
         return 1;
     }
-    bool sort = true, cpu = false, gpu = true, bvh = true;
+    bool sort = true, cpu = false, gpu = true, bvh = true, gpu_bvh = false;
     int devices = 1, device = 0;
     const char *asset_root = nullptr, *out_path = "raytracing.png", *stats_path = nullptr;
     rt_load_opts lo;
@@ -111,6 +111,7 @@ int main(int argc, char **argv) {
         else if (a == "--asset-root" && i + 1 < argc) asset_root = argv[++i];
         else if (a == "--out" && i + 1 < argc) out_path = argv[++i];
         else if (a == "--stats" && i + 1 < argc) stats_path = argv[++i];
+        else if (a == "--gpu-bvh") gpu_bvh = true;
         // unknown words are ignored, like the reference
     }
     if (!cpu && !gpu) {
@@ -130,6 +131,7 @@ int main(int argc, char **argv) {
         });
     lo.use_bvh = bvh ? 1 : 0;
     lo.asset_root = asset_root;
+    if (gpu_bvh) lo.bvh_device = device;          // GPU binned-SAH build, same node array
     rt_scene_host *host = nullptr;
     if (rt_scene_load(argv[1], &lo, &host)) return die("load_scene");
     const rt_scene *s = rt_scene_view(host);

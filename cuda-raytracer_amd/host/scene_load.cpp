@@ -31,6 +31,10 @@ int fail(int code, const std::string &msg) {
     return code;
 }
 
+// GPU binned-SAH build (csrc/bvh_build.hip): same output as BvhBuilder below.
+int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vector<rt_bvh_node> &nodes,
+                  int max_depth, int device);
+
 namespace {
 
 // fminf/fmaxf as glibc implements them (the reference's host min/max, math.cuh:126-142).
@@ -367,6 +371,7 @@ extern "C" {
 void rt_default_load_opts(rt_load_opts *o) {
     std::memset(o, 0, sizeof(*o));
     o->use_bvh = 1;
+    o->bvh_device = -1;
 }
 
 int rt_scene_load(const char *path, const rt_load_opts *opts_in, rt_scene_host **out) {
@@ -498,8 +503,14 @@ int rt_scene_load(const char *path, const rt_load_opts *opts_in, rt_scene_host *
 
     // BVH (scene.cu:1002-1036), then the ray-tracing triangle representation.
     const auto t0 = std::chrono::high_resolution_clock::now();
-    BvhBuilder(s->triangles, s->material_indices.data() + s->spheres.size(), s->bvh)
-        .build(opts.use_bvh ? 30 : 0, bvh_threads());
+    if (opts.bvh_device >= 0) {
+        if (int rc = rtamd::gpu_build_bvh(s->triangles, s->material_indices.data() + s->spheres.size(), s->bvh,
+                                          opts.use_bvh ? 30 : 0, opts.bvh_device))
+            return bad(rc);
+    } else {
+        BvhBuilder(s->triangles, s->material_indices.data() + s->spheres.size(), s->bvh)
+            .build(opts.use_bvh ? 30 : 0, bvh_threads());
+    }
     const auto t1 = std::chrono::high_resolution_clock::now();
     s->bvh_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (!opts.quiet) {

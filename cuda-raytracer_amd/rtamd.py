@@ -51,7 +51,7 @@ class RtScene(C.Structure):
 class RtLoadOpts(C.Structure):
     _fields_ = [("use_bvh", I32), ("quiet", I32), ("asset_root", C.c_char_p), ("image_override", I32),
                 ("width", I32), ("height", I32), ("ray_count", I32), ("bounces", I32),
-                ("exposure_override", I32), ("exposure", C.c_float)]
+                ("exposure_override", I32), ("exposure", C.c_float), ("bvh_device", I32)]
 
 
 class RtOpts(C.Structure):
@@ -137,11 +137,14 @@ def device_count():
 class Scene:
     """A scene loaded by the product loader (rt_scene_load)."""
 
-    def __init__(self, path, use_bvh=True, asset_root=ASSETS, image=None, exposure=None, quiet=True):
+    def __init__(self, path, use_bvh=True, asset_root=ASSETS, image=None, exposure=None, quiet=True,
+                 bvh_device=-1):
+        """bvh_device >= 0 builds the BVH on that GPU (same arrays as the host build)."""
         L = lib()
         o = RtLoadOpts()
         L.rt_default_load_opts(C.byref(o))
         o.use_bvh = int(use_bvh)
+        o.bvh_device = int(bvh_device)
         o.quiet = int(quiet)
         self._root = asset_root.encode() if asset_root else None
         o.asset_root = self._root

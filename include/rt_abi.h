@@ -78,6 +78,8 @@ typedef struct {
     int32_t width, height, ray_count, bounces;
     int32_t exposure_override;
     float exposure;
+    int32_t bvh_device;       /* -1 = build the BVH on the host (default); >= 0 = on that HIP device
+                                 (same node array, triangle and material-index order)          */
 } rt_load_opts;
 
 typedef struct rt_scene_host rt_scene_host;   /* owns the arrays a rt_scene points into */
