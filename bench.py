@@ -50,6 +50,7 @@ CONFIGS = {
     "cornell": ("cornell.scene", 256, 256, 64, 4, True, True),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+TILE_ROWS = 8          # pixel-tile stripe height (--shard tiles; SURVEY §8e: interleaved 8-row stripes)
 
 
 def segment_bytes(st, spheres):
@@ -114,6 +115,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-counters", action="store_true", help="skip the byte-model counting rerun")
     ap.add_argument("--dist", action="store_true", help="use the torch.distributed path even at N=1")
+    ap.add_argument("--shard", choices=("passes", "tiles"), default="passes",
+                    help="multi-GPU decomposition: whole passes per GPU (exact in both sort modes) or "
+                         "8-row pixel stripes per GPU over every pass (exact with --no-sort only)")
+    ap.add_argument("--tile-share", type=int, default=0, metavar="N",
+                    help="1-GPU probe of --shard tiles: render only rank 0's stripes of an N-GPU split")
     args = ap.parse_args()
     # The JSON line is the only thing on stdout: native libraries (RCCL prints a version banner)
     # write to stdout too, so fd 1 is pointed at stderr and the line goes to a saved copy of it.
@@ -141,13 +147,18 @@ def main():
     scene_file, W, H, spp, bounces, sort, use_bvh = cfg
     if args.no_sort:
         sort = False
+    tiles = args.shard == "tiles" or args.tile_share > 1
+    if tiles and sort:
+        ap.error("--shard tiles needs --no-sort: with the reorder on, process seeds follow the global "
+                 "post-sort slot (raytracing.cu:89), which a pixel tile cannot know")
     import make_envmap
     make_envmap.ensure_envmap(os.path.join(REPO, "assets", "teapot", "textures", "envmap.pfm"))
     t_load = time.perf_counter()
     scene = rtamd.Scene(os.path.join(rtamd.ASSETS, scene_file), use_bvh=use_bvh, image=(W, H, spp, bounces))
     load_s = time.perf_counter() - t_load
     P = scene.passes
-    ren = rtamd.Renderer(scene, sort=sort, device=local)
+    tile_split = (args.tile_share, 0) if args.tile_share > 1 else (world, rank)
+    ren = rtamd.Renderer(scene, sort=sort, device=local, tiles=tile_split + (TILE_ROWS,) if tiles else None)
 
     px3 = W * H * 3
     frame = None
@@ -164,12 +175,17 @@ def main():
         accumulate_stats(ren.run(pass_begin=passes[0], count=len(passes), stride=stride,
                                  d_pass_sums=out.data_ptr()))
 
-    R = -(-P // world)                  # rounds (one pass per GPU each) per frame
+    # rounds (one pass per GPU each) per frame; pixel tiles: every GPU renders every pass
+    R = P if tiles else -(-P // world)
     full_frame = args.steps is None
     steps = R if full_frame else args.steps
     if use_dist:
         import rtamd_dist
-        frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, torch.device("cuda", local), render_passes)
+        if tiles:
+            frame = rtamd_dist.TileShardedFrame(dist, torch, W, H, torch.device("cuda", local),
+                                                lambda out: ren.copy_framebuffer(out.data_ptr()), rows=TILE_ROWS)
+        else:
+            frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, torch.device("cuda", local), render_passes)
 
     def barrier_sync():
         if use_dist:
@@ -183,7 +199,15 @@ def main():
         done = mine = 0
         while done < k:
             m = min(k - done, R)
-            if use_dist:
+            if tiles:
+                # every pass over this GPU's row stripes, then one RCCL gather of the owned rows
+                # to rank 0 (rtamd_dist.TileShardedFrame)
+                ren.clear()
+                accumulate_stats(ren.run(pass_begin=0, count=m, stride=1))
+                if use_dist:
+                    frame.run_all()
+                mine += m
+            elif use_dist:
                 # this rank's passes of those rounds in one renderer call, then one RCCL all-to-all
                 # of pixel slices to their owners, which add them in pass order, and a gather of the
                 # finished slices to rank 0 (rtamd_dist.PassShardedFrame)
@@ -279,15 +303,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "strong" if full_frame else "weak",
+            "scaling": "strong" if full_frame or tiles else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: reference scene + assets, procedural stand-in env map (assets missing upstream)",
             "config": {
                 "workload": workload,
-                "step": "one 20-spp pass (%d rays x %d bounces) per GPU; pass-sharded over GPUs" % (20 * W * H, bounces),
+                "step": ("one 20-spp pass (%d rays x %d bounces) over this GPU's %d-row pixel stripes; "
+                         "every GPU renders every pass" % (20 * W * H, bounces, TILE_ROWS)) if tiles else
+                        ("one 20-spp pass (%d rays x %d bounces) per GPU; pass-sharded over GPUs" % (20 * W * H, bounces)),
                 "timed": ("one full frame (%d passes)" % P) if full_frame else ("%d passes per GPU" % steps),
-                "parallelism": "pass-shard x%d + RCCL all-to-all/gather" % world if world > 1 else "single GPU",
+                "parallelism": ("pixel-tile x%d (%d-row stripes) + RCCL gather" % (world, TILE_ROWS) if tiles else
+                                "pass-shard x%d + RCCL all-to-all/gather" % world) if world > 1 else "single GPU",
                 "nominal_mrays_per_s": round(nominal, 2),
                 "render_wall_ms": round(elapsed * 1e3, 1) if full_frame else None,
                 "render_wall_ms_projected": round(ms_step * R, 1),
@@ -296,6 +323,8 @@ def main():
                 "sort_ms_per_step": round(timed.get("sort_ms", 0.0) / max(my_passes, 1), 3),
                 "scene_load_s": round(load_s, 3),
                 "bvh_ms": round(scene.bvh_ms, 1),
+                **({"tile_share_probe": "rank 0's %d-row stripes of a %d-GPU split, on one GPU"
+                    % (TILE_ROWS, args.tile_share)} if args.tile_share > 1 else {}),
             },
             "roofline": roof,
             "cpu_baseline": None,

@@ -136,10 +136,27 @@ struct FastDiv {
     __device__ __forceinline__ uint32_t div(uint32_t n) const { return l == 0 ? n : (__umulhi(n, m) >> (l - 1)); }
 };
 
+// Bounce-0 slot -> global ray index (pixel * rtc + sample).  The whole image: the identity.
+// Pixel-tile sharding (rt_opts.tile_*): the pass's slots are this owner's row stripes back to
+// back, stripe j of the owner being global stripe j * tile_count + tile_index, so
+//   ray = slot + (slot / stripe) * (tile_count - 1) * stripe + tile_index * stripe.
+// Later bounces carry the ray index in rid[].  The same map on pixels (stripe = rows * W)
+// serves accumulation.
+struct SlotMap {
+    FastDiv by_stripe;
+    uint32_t skip, base;              // (tile_count - 1) * stripe, tile_index * stripe
+    static SlotMap identity() { return SlotMap{FastDiv::of(0x7fffffffu), 0u, 0u}; }
+    static SlotMap of(uint32_t stripe, int count, int index) {
+        return SlotMap{FastDiv::of(stripe), (uint32_t)(count - 1) * stripe, (uint32_t)index * stripe};
+    }
+    __device__ __forceinline__ uint32_t ray(uint32_t s) const { return s + by_stripe.div(s) * skip + base; }
+};
+
 struct PassArgs {
     int rtc;                          // rays per pixel this pass
     uint32_t gen_seed_term;           // 709579 * remaining (scene.cu:81)
     FastDiv by_rtc, by_width;         // ray index -> pixel -> row
+    SlotMap map;                      // bounce-0 slot -> ray index
 };
 
 __device__ __forceinline__ V3 primary_dir(const DevScene &S, int i, const PassArgs &pa) {
@@ -271,7 +288,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     nlive++;
                     if (FIRST) {
                         o = S.cam;
-                        d = primary_dir(S, slot, pa);
+                        d = primary_dir(S, (int)pa.map.ray((uint32_t)slot), pa);
                     } else {
                         const float4 *rp = geo + (size_t)slot * 2;   // ray state is in slot order
                         const float4 r0 = rp[0];
@@ -451,8 +468,10 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
         const int slot = base + threadIdx.x;
         if (slot >= L) continue;
         // The seed follows the reference's slot (raytracing.cu:89): the position with sort on;
-        // with sort off a ray keeps its original slot, which is its ray id.
-        const uint32_t seed_slot = (SORTED || FIRST) ? (uint32_t)slot : rid[slot];
+        // with sort off a ray keeps its original slot, which is its ray id.  At bounce 0 the
+        // reference slot is the ray id (pixel-tile renders: mapped from this tile's slot).
+        const uint32_t ray0 = FIRST ? pa.map.ray((uint32_t)slot) : 0u;
+        const uint32_t seed_slot = FIRST ? ray0 : (SORTED ? (uint32_t)slot : rid[slot]);
         Rng rng = pcg_seed(seed_slot * 4137874753u + seed_term);
         const float2 h = hits[slot];
         const float closest = h.x;
@@ -460,7 +479,7 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
         V3 o, d, T, C;
         if (FIRST) {
             o = S.cam;
-            d = primary_dir(S, slot, pa);
+            d = primary_dir(S, (int)ray0, pa);
             // T is laundered through an empty asm: with T a compile-time (1,1,1) the gfx950
             // backend dropped T.xy on the dielectric-reflect path of scatter (ROCm 7.2 clang;
             // T.xy came out as stale registers while T.z was right).  Keeping T opaque gives the
@@ -501,7 +520,7 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
             geo[(size_t)slot * 2] = make_float4(no.x, no.y, no.z, nd.x);
             geo[(size_t)slot * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
         }
-        if (dead || last) acc[FIRST ? (uint32_t)slot : rid[slot]] = tcv;
+        if (dead || last) acc[FIRST ? ray0 : rid[slot]] = tcv;
         else tc[slot] = tcv;
         if (!last) bkt[slot] = (uint8_t)(dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u));
     }
@@ -611,7 +630,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
                                                               const uint32_t *__restrict__ offsets,
                                                               const uint32_t *__restrict__ totals,
                                                               float4 *__restrict__ geo_out, float4 *__restrict__ tc_out,
-                                                              uint32_t *__restrict__ rid_out) {
+                                                              uint32_t *__restrict__ rid_out, SlotMap map) {
     const int n = (int)*live_count;
     if ((int)blockIdx.x * kSortTile >= n) return;
     __shared__ uint32_t run[kBuckets];
@@ -638,7 +657,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
             g0 = geo_in[(size_t)item * 2];
             g1 = geo_in[(size_t)item * 2 + 1];
             t = tc_in[item];
-            id = FIRST_SRC ? (uint32_t)item : rid_in[item];
+            id = FIRST_SRC ? map.ray((uint32_t)item) : rid_in[item];
         }
         const unsigned long long peers = match_bucket(b, valid);
         const uint32_t rank = rank_below(peers);
@@ -668,15 +687,18 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
 // A block stages the samples of kAccPixels consecutive pixels (contiguous in tc, pixel-major)
 // through LDS with coalesced loads, then one lane per pixel sums them in sample order.
 constexpr int kAccPixels = 64;
+// TILED: the block's pixels are tile pixels (this owner's row stripes back to back), mapped to
+// image pixels by `pix`; otherwise pixels of the whole image.
+template <bool TILED>
 __global__ __launch_bounds__(kBlock) void accumulate_kernel(const float4 *__restrict__ tc, int rtc, int pixels,
-                                                            float *__restrict__ sums) {
+                                                            float *__restrict__ sums, SlotMap pix) {
     __shared__ float col[kAccPixels * 20 * 3];
     const int p0 = blockIdx.x * kAccPixels;
     const int np = min(kAccPixels, pixels - p0);
     const int n = np * rtc;
     const float4 *src = tc + (size_t)p0 * rtc;
     for (int e = threadIdx.x; e < n; e += kBlock) {
-        const float4 c = src[e];
+        const float4 c = TILED ? tc[(size_t)pix.ray((uint32_t)(p0 + e / rtc)) * rtc + e % rtc] : src[e];
         col[e * 3] = c.y;
         col[e * 3 + 1] = c.z;
         col[e * 3 + 2] = c.w;
@@ -691,7 +713,7 @@ __global__ __launch_bounds__(kBlock) void accumulate_kernel(const float4 *__rest
         sy = sy + r[s * 3 + 1];
         sz = sz + r[s * 3 + 2];
     }
-    const size_t p = (size_t)(p0 + t);
+    const size_t p = TILED ? (size_t)pix.ray((uint32_t)(p0 + t)) : (size_t)(p0 + t);
     sums[p * 3] = sx;
     sums[p * 3 + 1] = sy;
     sums[p * 3 + 2] = sz;
@@ -835,6 +857,7 @@ struct PassCtx {
 struct rt_renderer {
     int device = 0;
     bool sort = true, counters = false;
+    int tile_count = 1, tile_index = 0, tile_rows = 8;   // pixel-tile sharding (rt_opts)
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
     DevBuf<float4> spheres, tris, mats, nodes;
@@ -855,12 +878,29 @@ struct rt_renderer {
 
     hipStream_t stream() const { return ctx[0].stream; }
     int pass_count() const { return (spp + 19) / 20; }
+    bool tiled() const { return tile_count > 1; }
+    // Pixels of this owner's stripes (the last stripe of the image may be short).
+    int64_t tile_pixels() const {
+        if (!tiled()) return (int64_t)width * height;
+        int64_t rows = 0;
+        for (int k = tile_index; (int64_t)k * tile_rows < height; k += tile_count)
+            rows += std::min(tile_rows, height - k * tile_rows);
+        return rows * width;
+    }
 
     // passes = false: scene only (rt_trace_rays), no pass contexts
     int init(const rt_scene *sc, const rt_opts *o, bool passes = true) {
         device = o->device;
         sort = o->sort != 0;
         counters = o->collect_counters != 0;
+        tile_count = std::max(1, o->tile_count);
+        tile_index = o->tile_index;
+        tile_rows = o->tile_rows > 0 ? o->tile_rows : 8;
+        if (tile_index < 0 || tile_index >= tile_count)
+            return rtamd::fail(RT_E_INVALID, "tile_index outside [0, tile_count)");
+        if (tile_count > 1 && sort)
+            return rtamd::fail(RT_E_INVALID, "pixel-tile sharding needs sort off: with the reorder on, process seeds "
+                                             "follow the global post-sort slot (raytracing.cu:89)");
         width = sc->width;
         height = sc->height;
         spp = sc->ray_count;
@@ -1014,15 +1054,30 @@ struct rt_renderer {
         const int rtc = std::min(before, 20);
         const int remaining = before - rtc;
         const int64_t pixels = (int64_t)width * height;
-        const int n = (int)(rtc * pixels);
+        const int64_t tpix = tile_pixels();     // pixels this render casts rays for
+        const int n = (int)(rtc * tpix);
         const int grid = blocks_for(n);
         const int tiles = (n + kSortTile - 1) / kSortTile;
         const int tgrid = std::min(grid, trace_blocks);
         const int sgrid = std::min(grid, cus * 8);
         hipStream_t st = c.stream;
         int cur = 0;
+        if (n == 0) {                           // a tile owner with no stripe of this image
+            for (int b = 0; b < bounces; b++) { // empty event pairs keep the stats bookkeeping aligned
+                hipEvent_t e0 = c.event(), e1 = c.event();
+                if (!e0 || !e1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
+                HIPCHK(hipEventRecord(e0, st));
+                HIPCHK(hipEventRecord(e1, st));
+            }
+            HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
+            return RT_OK;
+        }
         hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1, c.queue.p);
-        const PassArgs pa{rtc, 709579u * (uint32_t)remaining, FastDiv::of((uint32_t)rtc), FastDiv::of((uint32_t)width)};
+        const uint32_t stripe_px = (uint32_t)(tile_rows * width);
+        const SlotMap pix = tiled() ? SlotMap::of(stripe_px, tile_count, tile_index) : SlotMap::identity();
+        const SlotMap map = tiled() ? SlotMap::of(stripe_px * (uint32_t)rtc, tile_count, tile_index) : SlotMap::identity();
+        const PassArgs pa{rtc, 709579u * (uint32_t)remaining, FastDiv::of((uint32_t)rtc), FastDiv::of((uint32_t)width),
+                          map};
         for (int b = 0; b < bounces; b++) {
             const uint32_t seed_term = 279220567u * (uint32_t)(remaining * 20 + b);
             hipEvent_t e0 = c.event(), e1 = c.event();
@@ -1065,11 +1120,11 @@ struct rt_renderer {
                 if (b == 0)
                     hipLaunchKernelGGL(sort_scatter_kernel<true>, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
                                        c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p);
+                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
                 else
                     hipLaunchKernelGGL(sort_scatter_kernel<false>, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
                                        c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p);
+                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventRecord(s1, st));
                 cur = 1 - cur;
@@ -1079,9 +1134,15 @@ struct rt_renderer {
         if (bounces == 0) {
             // rays were generated with collected = 0 and never processed (raytracing.cu:232)
             HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
+        } else if (!tiled()) {
+            hipLaunchKernelGGL(accumulate_kernel<false>, dim3((unsigned)((pixels + kAccPixels - 1) / kAccPixels)),
+                               dim3(kBlock), 0, st, c.acc.p, rtc, (int)pixels, sums, pix);
         } else {
-            hipLaunchKernelGGL(accumulate_kernel, dim3((unsigned)((pixels + kAccPixels - 1) / kAccPixels)), dim3(kBlock),
-                               0, st, c.acc.p, rtc, (int)pixels, sums);
+            // other owners' pixels stay 0 in this render's pass sums
+            HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
+            if (tpix > 0)
+                hipLaunchKernelGGL(accumulate_kernel<true>, dim3((unsigned)((tpix + kAccPixels - 1) / kAccPixels)),
+                                   dim3(kBlock), 0, st, c.acc.p, rtc, (int)tpix, sums, pix);
         }
         HIPCHK(hipGetLastError());
         return RT_OK;
@@ -1112,7 +1173,7 @@ struct rt_renderer {
         const uint32_t nn = (uint32_t)n;
         HIPCHK(hipMemcpyAsync(live.p, &nn, sizeof(nn), hipMemcpyHostToDevice, s0));
         HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, s0));
-        const PassArgs pa{1, 0u, FastDiv::of(1), FastDiv::of((uint32_t)width)};
+        const PassArgs pa{1, 0u, FastDiv::of(1), FastDiv::of((uint32_t)width), SlotMap::identity()};
         const int tgrid = std::min(blocks_for(n), trace_blocks);
         if (counters)
             hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
@@ -1170,7 +1231,7 @@ struct rt_renderer {
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c.fb_done, c.stream));
             prev_fb = c.fb_done;
-            generated += (int64_t)std::min(spp - 20 * p, 20) * width * height;
+            generated += (int64_t)std::min(spp - 20 * p, 20) * tile_pixels();
         }
         for (int k = 1; k < inflight; k++) {
             HIPCHK(hipEventRecord(ctx[k].done, ctx[k].stream));
@@ -1353,6 +1414,14 @@ int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out) {
     if (!r || !fb_out) return rtamd::fail(RT_E_INVALID, "null argument");
     HIPCHK(hipSetDevice(r->device));
     HIPCHK(hipMemcpyAsync(fb_out, r->fb.p, r->fb.n * sizeof(float), hipMemcpyDeviceToHost, r->stream()));
+    HIPCHK(hipStreamSynchronize(r->stream()));
+    return RT_OK;
+}
+
+int rt_renderer_copy_framebuffer(rt_renderer *r, float *d_out) {
+    if (!r || !d_out) return rtamd::fail(RT_E_INVALID, "null argument");
+    HIPCHK(hipSetDevice(r->device));
+    HIPCHK(hipMemcpyAsync(d_out, r->fb.p, r->fb.n * sizeof(float), hipMemcpyDeviceToDevice, r->stream()));
     HIPCHK(hipStreamSynchronize(r->stream()));
     return RT_OK;
 }

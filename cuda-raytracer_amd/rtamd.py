@@ -56,7 +56,8 @@ class RtLoadOpts(C.Structure):
 
 class RtOpts(C.Structure):
     _fields_ = [("sort", I32), ("device", I32), ("pass_begin", I32), ("pass_count", I32),
-                ("pass_stride", I32), ("collect_counters", I32)]
+                ("pass_stride", I32), ("collect_counters", I32),
+                ("tile_count", I32), ("tile_index", I32), ("tile_rows", I32)]
 
 
 class RtStats(C.Structure):
@@ -103,6 +104,7 @@ def lib():
         L.rt_renderer_run.argtypes = [P, I32, I32, I32, P, P]
         L.rt_renderer_run_host.argtypes = [P, I32, I32, I32, P, P]
         L.rt_renderer_read_framebuffer.argtypes = [P, P]
+        L.rt_renderer_copy_framebuffer.argtypes = [P, P]
         L.rt_renderer_clear.argtypes = [P]
         L.rt_renderer_set_counters.argtypes = [P, I32]
         L.rt_renderer_destroy.argtypes = [P]
@@ -213,19 +215,33 @@ class Scene:
                     camera=cam)
 
 
-def default_opts(sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=1, counters=False):
+def default_opts(sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=1, counters=False,
+                 tiles=None):
+    """tiles = (tile_count, tile_index[, tile_rows]): render only that owner's row stripes."""
     o = RtOpts()
     lib().rt_default_opts(C.byref(o))
     o.sort, o.device, o.pass_begin, o.pass_count = int(sort), device, pass_begin, pass_count
     o.pass_stride, o.collect_counters = pass_stride, int(counters)
+    if tiles is not None:
+        o.tile_count, o.tile_index = tiles[0], tiles[1]
+        o.tile_rows = tiles[2] if len(tiles) > 2 else 0
     return o
 
 
-def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=1, counters=False):
+def tile_rows_of(height, tile_count, tile_index, tile_rows=8):
+    """Image rows owned by tile_index: stripes of tile_rows rows dealt round-robin (rt_opts)."""
+    rows = []
+    for k in range(tile_index, -(-height // tile_rows), tile_count):
+        rows.extend(range(k * tile_rows, min((k + 1) * tile_rows, height)))
+    return rows
+
+
+def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=1, counters=False,
+           tiles=None):
     """rt_render: the drop-in for gpu_raytrace.  Returns (framebuffer W*H*3 float32, stats)."""
     fb = np.zeros(scene.pixels * 3, np.float32)
     st = RtStats()
-    o = default_opts(sort, device, pass_begin, pass_count, pass_stride, counters)
+    o = default_opts(sort, device, pass_begin, pass_count, pass_stride, counters, tiles)
     _check(lib().rt_render(scene.ptr, C.byref(o), _ptr(fb), C.byref(st)))
     return fb, st.as_dict()
 
@@ -245,9 +261,9 @@ def trace_rays(scene, rays, device=0, counters=False):
 class Renderer:
     """Persistent renderer (scene + ray buffers resident in HBM)."""
 
-    def __init__(self, scene, sort=True, device=0, counters=False):
+    def __init__(self, scene, sort=True, device=0, counters=False, tiles=None):
         self.scene = scene
-        o = default_opts(sort, device, counters=counters)
+        o = default_opts(sort, device, counters=counters, tiles=tiles)
         h = P()
         _check(lib().rt_renderer_create(scene.ptr, C.byref(o), C.byref(h)))
         self.h = h
@@ -272,6 +288,10 @@ class Renderer:
         fb = np.zeros(self.scene.pixels * 3, np.float32)
         _check(lib().rt_renderer_read_framebuffer(self.h, _ptr(fb)))
         return fb
+
+    def copy_framebuffer(self, d_out):
+        """Device framebuffer -> device pointer d_out (W*H*3 float32 on the renderer's device)."""
+        _check(lib().rt_renderer_copy_framebuffer(self.h, P(d_out)))
 
     def clear(self):
         _check(lib().rt_renderer_clear(self.h))

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum {
     RT_OK = 0,
@@ -100,6 +100,15 @@ typedef struct {
     int32_t pass_count;   /* passes to render; -1 = all remaining                        */
     int32_t pass_stride;  /* render passes pass_begin, +stride, ... (multi-GPU pass shard) */
     int32_t collect_counters; /* 1 = also count traversal work (Pn/Iv/Tt) for the byte model */
+    /* Pixel-tile sharding: the image is cut into stripes of tile_rows rows, dealt
+     * round-robin to tile_count owners; this render casts only the rays of owner tile_index's
+     * stripes, with their global ray indices (so seeds are the 1-GPU ones), and leaves the other
+     * pixels 0.  Exact only with sort = 0: with the reorder on, process seeds follow the global
+     * post-sort slot (raytracing.cu:89, :238-247), which a tile cannot know; sort = 1 with
+     * tile_count > 1 is RT_E_INVALID.  tile_count 0 or 1 = the whole image (default). */
+    int32_t tile_count;
+    int32_t tile_index;
+    int32_t tile_rows;    /* stripe height in rows; 0 = 8 */
 } rt_opts;
 
 typedef struct {
@@ -150,6 +159,8 @@ int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t s
 int rt_renderer_run_host(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride,
                          float *host_pass_sums, rt_stats *stats);
 int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out);   /* device fb -> host     */
+int rt_renderer_copy_framebuffer(rt_renderer *r, float *d_out);    /* device fb -> device ptr on
+                                                                       r's device (W*H*3 floats) */
 int rt_renderer_clear(rt_renderer *r);                               /* zero the device fb    */
 int rt_renderer_set_counters(rt_renderer *r, int32_t enable);
 void rt_renderer_destroy(rt_renderer *r);

@@ -40,16 +40,27 @@ def test_library_is_gfx950_and_links_hip():
 def test_struct_layouts():
     # sizes fixed by the reference layouts (scene.cuh:9-100) and by rt_abi.h
     assert C.sizeof(R.RtScene) == 216
-    assert C.sizeof(R.RtOpts) == 24
+    assert C.sizeof(R.RtOpts) == 36   # + tile_count, tile_index, tile_rows
     assert C.sizeof(R.RtLoadOpts) == 48
     assert C.sizeof(R.RtStats) == 11 * 8 + 8 + 4 * 8
-    assert R.lib().rt_abi_version() == 1
+    assert R.lib().rt_abi_version() == 2
 
 
 def test_default_options():
     o = R.RtOpts()
     R.lib().rt_default_opts(C.byref(o))
     assert (o.sort, o.device, o.pass_begin, o.pass_count, o.pass_stride, o.collect_counters) == (1, 0, 0, -1, 1, 0)
+    assert (o.tile_count, o.tile_index, o.tile_rows) == (0, 0, 0)   # whole image, 8-row stripes
+
+
+def test_tile_rows_of():
+    # 8-row stripes dealt round-robin; the image's last stripe may be short
+    assert R.tile_rows_of(20, 2, 0) == list(range(0, 8)) + list(range(16, 20))
+    assert R.tile_rows_of(20, 2, 1) == list(range(8, 16))
+    assert R.tile_rows_of(20, 4, 3) == []
+    for h, t, r in ((1080, 8, 8), (37, 3, 5), (9, 5, 2)):
+        rows = sorted(x for i in range(t) for x in R.tile_rows_of(h, t, i, r))
+        assert rows == list(range(h))
 
 
 def test_invalid_arguments_fail_loudly():

@@ -1,0 +1,82 @@
+"""Pixel-tile sharding (rt_opts.tile_*): a render restricted to one owner's row
+stripes, with sort off, equals the whole-image render on those rows bit for bit and leaves the
+other rows 0, so the owners' images add up to the 1-GPU image exactly.  With sort on a tile
+cannot know the global post-sort slots the process seeds follow (raytracing.cu:89), and the
+renderer refuses it."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import rtamd as R
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # scene, image (W, H, spp, bounces), tile_count, tile_rows
+    ("cornell", (64, 64, 24, 4), 3, 8),
+    ("teapot", (96, 54, 20, 16), 2, 8),        # 54 rows: the last stripe is 6 rows
+    ("lamp_available", (80, 45, 20, 32), 4, 5),
+    ("spheres", (33, 17, 7, 1), 5, 2),         # odd sizes, partial pass, short last stripe
+    ("cornell_plus", (48, 20, 20, 8), 4, 8),   # 3 stripes over 4 owners: owner 3 has none
+]
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if R.device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on the MI355X box")
+    return 0
+
+
+@pytest.mark.parametrize("scene,image,count,rows", CASES)
+def test_tile_shares_equal_full_render(gpu, scene, image, count, rows):
+    path = "%s/%s.scene" % (R.ASSETS, scene)
+    psc = R.Scene(path, image=image)
+    W, H = image[0], image[1]
+    full, fst = R.render(psc, sort=False)
+    total = np.zeros_like(full)
+    gen = live = 0
+    for i in range(count):
+        fb, st = R.render(psc, sort=False, tiles=(count, i, rows))
+        img = fb.reshape(H, W, 3)
+        mine = R.tile_rows_of(H, count, i, rows)
+        other = sorted(set(range(H)) - set(mine))
+        assert np.array_equal(img[mine], full.reshape(H, W, 3)[mine])
+        assert not img[other].any()
+        total += fb                              # x + 0 = x: the owners' images add exactly
+        gen += st["generated_rays"]
+        live += st["live_segments"]
+    assert np.array_equal(total, full)
+    assert gen == fst["generated_rays"]
+    assert live == fst["live_segments"]
+
+
+def test_tile_share_matches_oracle_rows(gpu):
+    path = "%s/teapot.scene" % R.ASSETS
+    image = (96, 54, 20, 16)
+    ofb, _ = O.OracleScene(path, image=image).render(sort=False)
+    fb, _ = R.render(R.Scene(path, image=image), sort=False, tiles=(3, 1, 8))
+    rows = R.tile_rows_of(54, 3, 1, 8)
+    assert np.array_equal(fb.reshape(54, 96, 3)[rows], ofb.reshape(54, 96, 3)[rows])
+
+
+def test_tile_renderer_passes_in_flight(gpu):
+    # the persistent renderer with several passes in flight, and stride-sharded passes
+    path = "%s/teapot.scene" % R.ASSETS
+    image = (64, 40, 100, 8)
+    psc = R.Scene(path, image=image)
+    full, _ = R.render(psc, sort=False)
+    ren = R.Renderer(psc, sort=False, tiles=(2, 0, 8))
+    ren.run(0, psc.passes, 1)
+    fb = ren.framebuffer()
+    ren.close()
+    rows = R.tile_rows_of(40, 2, 0, 8)
+    assert np.array_equal(fb.reshape(40, 64, 3)[rows], full.reshape(40, 64, 3)[rows])
+
+
+def test_tiles_with_sort_on_are_refused(gpu):
+    psc = R.Scene("%s/cornell.scene" % R.ASSETS, image=(32, 32, 4, 2))
+    with pytest.raises(R.RtError, match="sort off"):
+        R.render(psc, sort=True, tiles=(2, 0))
+    with pytest.raises(R.RtError, match="tile_index"):
+        R.render(psc, sort=False, tiles=(2, 2))

@@ -57,3 +57,40 @@ def test_schedule_covers_every_pass_once():
         for passes in (1, 5, 103, 205):
             got = sorted(p for r in range(world) for p in D.pass_schedule(r, world, passes))
             assert got == list(range(passes))
+
+
+def _tile_worker(rank, world, port, out_path, rows):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = O.OracleScene(os.path.join(O.ASSETS, "cornell_plus.scene"), image=IMAGE)
+    W, H = IMAGE[0], IMAGE[1]
+
+    def render_tile(out):
+        # the tile render equals the full render on the owned rows and is 0 elsewhere
+        # (tests/test_gpu_tiles.py checks that of the HIP path); the oracle stands in for it here
+        full = sc.render(sort=False, threads=2)[0].reshape(H, W * 3)
+        mask = np.zeros((H, 1), np.float32)
+        mask[D.tile_rows(H, world, rank, rows)] = 1
+        out.copy_(torch.from_numpy(full * mask))
+
+    frame = D.TileShardedFrame(dist, torch, W, H, "cpu", render_tile, rows=rows)
+    fb = frame.run_all()
+    if rank == 0:
+        np.save(out_path, fb.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,rows", [(2, 8), (3, 3), (4, 8)])   # (4, 8): 2 stripes, ranks 2-3 own none
+def test_tile_sharded_frame_is_bitexact(tmp_path, world, rows):
+    out = str(tmp_path / "fb.npy")
+    mp.spawn(_tile_worker, args=(world, _free_port(), out, rows), nprocs=world, join=True)
+    got = np.load(out)
+    ref, _ = O.OracleScene(os.path.join(O.ASSETS, "cornell_plus.scene"), image=IMAGE).render(sort=False)
+    assert np.array_equal(got, ref)
+
+
+def test_tile_rows_cover_the_image_once():
+    for world in (1, 2, 3, 8):
+        for h, rows in ((1080, 8), (512, 8), (17, 3), (5, 8)):
+            got = sorted(y for r in range(world) for y in D.tile_rows(h, world, r, rows))
+            assert got == list(range(h))
