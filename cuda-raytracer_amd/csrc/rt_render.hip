@@ -152,6 +152,14 @@ struct SlotMap {
     __device__ __forceinline__ uint32_t ray(uint32_t s) const { return s + by_stripe.div(s) * skip + base; }
 };
 
+// Bounce-0 kernels come in two flavours: FIRST == 1 (whole image, slot = ray index) and
+// FIRST == 2 (pixel tile, mapped); later bounces are FIRST == 0.  Keeping the map out of the
+// whole-image kernels keeps their code (and registers) as they were.
+template <int FIRST>
+__device__ __forceinline__ uint32_t first_ray(const SlotMap &m, uint32_t slot) {
+    return FIRST == 2 ? m.ray(slot) : slot;
+}
+
 struct PassArgs {
     int rtc;                          // rays per pixel this pass
     uint32_t gen_seed_term;           // 709579 * remaining (scene.cu:81)
@@ -221,7 +229,7 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #define RT_TRACE_WPE 8
 #endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, 8)))
-template <bool SORTED, bool COUNT, bool FIRST>
+template <bool SORTED, bool COUNT, int FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
@@ -288,7 +296,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     nlive++;
                     if (FIRST) {
                         o = S.cam;
-                        d = primary_dir(S, (int)pa.map.ray((uint32_t)slot), pa);
+                        d = primary_dir(S, (int)first_ray<FIRST>(pa.map, (uint32_t)slot), pa);
                     } else {
                         const float4 *rp = geo + (size_t)slot * 2;   // ray state is in slot order
                         const float4 r0 = rp[0];
@@ -455,7 +463,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 // Ray state lives in slot order (the reorder moves it), so every access here is coalesced.  A
 // ray's radiance goes to acc[ray id] (pixel-major, what accumulation reads) when it terminates
 // or after the last bounce.
-template <bool SORTED, bool COUNT, bool FIRST>
+template <bool SORTED, bool COUNT, int FIRST>
 __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
                                                        float4 *__restrict__ tc, const uint32_t *__restrict__ rid,
                                                        float4 *__restrict__ acc, uint8_t *__restrict__ bkt,
@@ -470,8 +478,8 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
         // The seed follows the reference's slot (raytracing.cu:89): the position with sort on;
         // with sort off a ray keeps its original slot, which is its ray id.  At bounce 0 the
         // reference slot is the ray id (pixel-tile renders: mapped from this tile's slot).
-        const uint32_t ray0 = FIRST ? pa.map.ray((uint32_t)slot) : 0u;
-        const uint32_t seed_slot = FIRST ? ray0 : (SORTED ? (uint32_t)slot : rid[slot]);
+        const uint32_t ray0 = first_ray<FIRST>(pa.map, (uint32_t)slot);   // bounce 0 only
+        const uint32_t seed_slot = (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
         Rng rng = pcg_seed(seed_slot * 4137874753u + seed_term);
         const float2 h = hits[slot];
         const float closest = h.x;
@@ -479,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
         V3 o, d, T, C;
         if (FIRST) {
             o = S.cam;
-            d = primary_dir(S, (int)ray0, pa);
+            d = primary_dir(S, FIRST == 2 ? (int)ray0 : slot, pa);
             // T is laundered through an empty asm: with T a compile-time (1,1,1) the gfx950
             // backend dropped T.xy on the dielectric-reflect path of scatter (ROCm 7.2 clang;
             // T.xy came out as stale registers while T.z was right).  Keeping T opaque gives the
@@ -520,7 +528,7 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
             geo[(size_t)slot * 2] = make_float4(no.x, no.y, no.z, nd.x);
             geo[(size_t)slot * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
         }
-        if (dead || last) acc[FIRST ? ray0 : rid[slot]] = tcv;
+        if (dead || last) acc[FIRST ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot]] = tcv;
         else tc[slot] = tcv;
         if (!last) bkt[slot] = (uint8_t)(dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u));
     }
@@ -621,7 +629,7 @@ __global__ __launch_bounds__(kBlock) void sort_scan_kernel(const uint32_t *__res
 // earlier lanes holding the same bucket.  Live rays move with their state (geometry, T/C, ray
 // id) so that the next bounce reads them in slot order; terminated rays (bucket 64, last in the
 // order) have already delivered their radiance and are dropped.  At bounce 0 slot = ray id.
-template <bool FIRST_SRC>
+template <int FIRST_SRC>
 __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__restrict__ bkt_in,
                                                               const float4 *__restrict__ geo_in,
                                                               const float4 *__restrict__ tc_in,
@@ -657,7 +665,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
             g0 = geo_in[(size_t)item * 2];
             g1 = geo_in[(size_t)item * 2 + 1];
             t = tc_in[item];
-            id = FIRST_SRC ? map.ray((uint32_t)item) : rid_in[item];
+            id = FIRST_SRC ? first_ray<FIRST_SRC>(map, (uint32_t)item) : rid_in[item];
         }
         const unsigned long long peers = match_bucket(b, valid);
         const uint32_t rank = rank_below(peers);
@@ -1096,12 +1104,14 @@ struct rt_renderer {
     } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
     do {                                                                                                         \
-        if (b == 0) RT_PROCESS3(SORTED, COUNT, true); else RT_PROCESS3(SORTED, COUNT, false);                     \
+        if (b == 0) RT_PROCESS3(SORTED, COUNT, 1); else RT_PROCESS3(SORTED, COUNT, 0);                           \
     } while (0)
             if (sort) {
                 if (counters) RT_PROCESS(true, true); else RT_PROCESS(true, false);
             } else {
-                if (counters) RT_PROCESS(false, true); else RT_PROCESS(false, false);
+                if (b == 0 && tiled()) {        // pixel tile (sort off only): mapped bounce-0 slots
+                    if (counters) RT_PROCESS3(false, true, 2); else RT_PROCESS3(false, false, 2);
+                } else if (counters) RT_PROCESS(false, true); else RT_PROCESS(false, false);
             }
 #undef RT_PROCESS
 #undef RT_PROCESS3
@@ -1117,12 +1127,16 @@ struct rt_renderer {
                                    c.sort_counts.p);
                 hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, lv, tiles,
                                    c.sort_offsets.p, c.sort_totals.p, c.live.p + b + 1);
-                if (b == 0)
-                    hipLaunchKernelGGL(sort_scatter_kernel<true>, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                if (b == 0 && tiled())
+                    hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
+                else if (b == 0)
+                    hipLaunchKernelGGL(sort_scatter_kernel<1>, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
                                        c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
                                        c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
                 else
-                    hipLaunchKernelGGL(sort_scatter_kernel<false>, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                    hipLaunchKernelGGL(sort_scatter_kernel<0>, dim3(tiles), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
                                        c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
                                        c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
                 HIPCHK(hipGetLastError());

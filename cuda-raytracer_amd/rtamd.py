@@ -104,7 +104,6 @@ def lib():
         L.rt_renderer_run.argtypes = [P, I32, I32, I32, P, P]
         L.rt_renderer_run_host.argtypes = [P, I32, I32, I32, P, P]
         L.rt_renderer_read_framebuffer.argtypes = [P, P]
-        L.rt_renderer_copy_framebuffer.argtypes = [P, P]
         L.rt_renderer_clear.argtypes = [P]
         L.rt_renderer_set_counters.argtypes = [P, I32]
         L.rt_renderer_destroy.argtypes = [P]
@@ -291,7 +290,9 @@ class Renderer:
 
     def copy_framebuffer(self, d_out):
         """Device framebuffer -> device pointer d_out (W*H*3 float32 on the renderer's device)."""
-        _check(lib().rt_renderer_copy_framebuffer(self.h, P(d_out)))
+        f = lib().rt_renderer_copy_framebuffer
+        f.argtypes = [P, P]
+        _check(f(self.h, P(d_out)))
 
     def clear(self):
         _check(lib().rt_renderer_clear(self.h))
