@@ -159,17 +159,46 @@ __global__ __launch_bounds__(kThreads) void bounds_kernel(const NodeRange *__res
         __syncthreads();
         float scale[3];
         for (int a = 0; a < 3; a++) scale[a] = kBins / (cmax[a] - cmin[a]);   // scene.cu:911
-        for (int i = lo + t; i < hi; i += kThreads) {
-            const float4 l = blo[i], h = bhi[i], ce = cen[i];
+        // Neighbouring triangles mostly share a bin, so per-lane atomics would serialise 64 ways on
+        // one LDS word: the lanes holding the same bin are found by ballot, reduced across the
+        // wave by shuffles, and one lane per (wave, bin) does the atomics.  The loop is
+        // wave-uniform (ballots need every lane).
+        for (int i0 = lo + (t & ~63); i0 < hi; i0 += kThreads) {
+            const int i = i0 + lane;
+            const bool valid = i < hi;
+            float4 l = make_float4(0, 0, 0, 0), h = l, ce = l;
+            if (valid) { l = blo[i]; h = bhi[i]; ce = cen[i]; }
             const float cc[3] = {ce.x, ce.y, ce.z};
+            const int kl[3] = {fkey(l.x), fkey(l.y), fkey(l.z)}, kh[3] = {fkey(h.x), fkey(h.y), fkey(h.z)};
             for (int a = 0; a < 3; a++) {
                 if (cmin[a] == cmax[a]) continue;
                 const int b = min(kBins - 1, (int)((cc[a] - cmin[a]) * scale[a]));   // scene.cu:918
-                atomicAdd(&s_wcnt[w][a][b], 1);
-                atomicMin(&s_wkey[w][a][b][0], fkey(l.x)); atomicMin(&s_wkey[w][a][b][1], fkey(l.y));
-                atomicMin(&s_wkey[w][a][b][2], fkey(l.z));
-                atomicMax(&s_wkey[w][a][b][3], fkey(h.x)); atomicMax(&s_wkey[w][a][b][4], fkey(h.y));
-                atomicMax(&s_wkey[w][a][b][5], fkey(h.z));
+                unsigned long long rem = __ballot(valid);
+                while (rem) {
+                    const int leader = __ffsll((long long)rem) - 1;
+                    const int b0 = __shfl(b, leader);
+                    const bool in = valid && b == b0;
+                    const unsigned long long m = __ballot(in);
+                    int r[6];
+                    for (int q = 0; q < 3; q++) {
+                        r[q] = in ? kl[q] : 0x7fffffff;
+                        r[q + 3] = in ? kh[q] : (int)0x80000000;
+                    }
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1)
+                        for (int q = 0; q < 3; q++) {
+                            r[q] = min(r[q], __shfl_xor(r[q], off));
+                            r[q + 3] = max(r[q + 3], __shfl_xor(r[q + 3], off));
+                        }
+                    if (lane == leader) {
+                        atomicAdd(&s_wcnt[w][a][b0], __popcll(m));
+                        for (int q = 0; q < 3; q++) {
+                            atomicMin(&s_wkey[w][a][b0][q], r[q]);
+                            atomicMax(&s_wkey[w][a][b0][q + 3], r[q + 3]);
+                        }
+                    }
+                    rem &= ~m;
+                }
             }
         }
         __syncthreads();
@@ -468,9 +497,8 @@ int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vecto
     BCHK(idx.alloc(m)); BCHK(t_idx.alloc(m)); BCHK(xk.alloc(m)); BCHK(rk.alloc(m)); BCHK(side.alloc(m));
     // a level holds at most n / 1 nodes (ranges are disjoint and non-empty below the root)
     BCHK(d_nodes.alloc(m)); BCHK(d_out.alloc(m));
-    hipStream_t s;
-    BCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    struct StreamGuard { hipStream_t s; ~StreamGuard() { (void)hipStreamDestroy(s); } } sg{s};
+    // the per-thread default stream: the build is synchronous, and a stream costs ~3.6 ms to create
+    hipStream_t s = hipStreamPerThread;
     BCHK(hipMemcpyAsync(blo.p, h_lo.data(), m * sizeof(float4), hipMemcpyHostToDevice, s));
     BCHK(hipMemcpyAsync(bhi.p, h_hi.data(), m * sizeof(float4), hipMemcpyHostToDevice, s));
     BCHK(hipMemcpyAsync(cen.p, h_cen.data(), m * sizeof(float4), hipMemcpyHostToDevice, s));
@@ -484,7 +512,9 @@ int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vecto
     std::vector<int> level{0};                   // tree indices of the current level
     std::vector<NodeRange> h_ranges;
     std::vector<NodeOut> h_out;
+    std::string levels_report;
     for (int depth = 0; !level.empty(); depth++) {
+        const auto t_level = clk::now();
         const int cnt = (int)level.size();
         // big nodes first (a 16-wave workgroup each), then the rest (one wave each)
         std::stable_partition(level.begin(), level.end(),
@@ -532,8 +562,15 @@ int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vecto
             next.push_back(c + 1);
         }
         level.swap(next);
+        if (timing) {
+            char buf[64];
+            std::snprintf(buf, sizeof(buf), " %d:%d/%d/%.2f", depth, cnt, nbig,
+                          std::chrono::duration<double, std::milli>(clk::now() - t_level).count());
+            levels_report += buf;
+        }
     }
     mark("levels");
+    if (timing) std::fprintf(stderr, "gpu_build_bvh levels (depth:nodes/big/ms):%s\n", levels_report.c_str());
     BCHK(hipMemcpyAsync(h_idx.data(), idx.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     BCHK(hipStreamSynchronize(s));
     // node numbering of the reference's recursion: a split allocates its two children at the
