@@ -222,6 +222,9 @@ def main():
             stats[key] = stats.get(key, 0) + v
         return mine
 
+    # No per-bounce HIP events in the timed steps (four marker packets per bounce in every pass's
+    # stream cost ~2 %); the kernel-time split comes from an untimed re-run below.
+    ren.set_event_timing(False)
     warm = {}
     run_steps(args.warmup, warm)
     barrier_sync()
@@ -232,7 +235,13 @@ def main():
     elapsed = time.perf_counter() - t0
 
     live = timed.get("live_segments", 0)
-    proc_ms = timed.get("process_ms", 0.0)
+    # Kernel-time split (process / reorder launches, HIP events on each pass's stream): the same
+    # steps again, untimed, with events on.
+    ren.set_event_timing(True)
+    evrun = {}
+    run_steps(steps, evrun)
+    ren.set_event_timing(False)
+    proc_ms = evrun.get("process_ms", 0.0)
     if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -283,6 +292,8 @@ def main():
                     "kernel": "process (trace_kernel + shade_kernel per bounce)",
                     "bytes_per_launch": int(bytes_launch), "ms_per_launch": round(ms_launch, 4),
                     "achieved_per_launch_events": round(per_launch, 1),
+                    "per_launch_events_from": "untimed re-run of the timed steps with per-bounce HIP events "
+                                              "(the timed steps record none)",
                     "model": "SURVEY.md 8(d): per live segment 108+16S + 32*Pn + 64*Iv + 48*Tt + hit(98|66)/miss(12); "
                              "dead slots: 0 B with sort (never visited), 1 B without; counts from the device "
                              "counters of the same passes; achieved = bytes of all process launches / timed wall"}
@@ -320,7 +331,7 @@ def main():
                 "render_wall_ms_projected": round(ms_step * R, 1),
                 "passes_per_frame": P,
                 "process_ms_per_step": round(proc_ms / max(my_passes, 1), 3),
-                "sort_ms_per_step": round(timed.get("sort_ms", 0.0) / max(my_passes, 1), 3),
+                "sort_ms_per_step": round(evrun.get("sort_ms", 0.0) / max(my_passes, 1), 3),
                 "scene_load_s": round(load_s, 3),
                 "bvh_ms": round(scene.bvh_ms, 1),
                 **({"tile_share_probe": "rank 0's %d-row stripes of a %d-GPU split, on one GPU"

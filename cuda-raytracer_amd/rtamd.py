@@ -283,6 +283,12 @@ class Renderer:
     def set_counters(self, on):
         _check(lib().rt_renderer_set_counters(self.h, int(on)))
 
+    def set_event_timing(self, on):
+        """Per-bounce HIP events for process_ms / sort_ms (default on; off is ~2 % faster)."""
+        f = lib().rt_renderer_set_event_timing
+        f.argtypes = [P, I32]
+        _check(f(self.h, int(on)))
+
     def framebuffer(self):
         fb = np.zeros(self.scene.pixels * 3, np.float32)
         _check(lib().rt_renderer_read_framebuffer(self.h, _ptr(fb)))
