@@ -461,6 +461,67 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 #endif
 }
 
+// One ray's shading (scene.cu:376-485) at `slot`: environment lookup on a miss, otherwise
+// emission + scatter.  Returns the new state; `ray` = the ray id (acc index), kind = 0 miss,
+// 1 triangle hit, 2 sphere hit.
+struct Shaded {
+    V3 no, nd, T, C;
+    uint32_t ray;
+    int kind;
+};
+template <bool SORTED, int FIRST>
+__device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &pa, int slot,
+                                            const float4 *__restrict__ geo, const float4 *__restrict__ tc,
+                                            const uint32_t *__restrict__ rid, const float2 *__restrict__ hits,
+                                            uint32_t seed_term) {
+    // The seed follows the reference's slot (raytracing.cu:89): the position with sort on;
+    // with sort off a ray keeps its original slot, which is its ray id.  At bounce 0 the
+    // reference slot is the ray id (pixel-tile renders: mapped from this tile's slot).
+    const uint32_t ray0 = first_ray<FIRST>(pa.map, (uint32_t)slot);   // bounce 0 only
+    const uint32_t seed_slot = (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
+    Rng rng = pcg_seed(seed_slot * 4137874753u + seed_term);
+    const float2 h = hits[slot];
+    const float closest = h.x;
+    const int index = __float_as_int(h.y);
+    V3 o, d, T, C;
+    if (FIRST) {
+        o = S.cam;
+        d = primary_dir(S, FIRST == 2 ? (int)ray0 : slot, pa);
+        // T is laundered through an empty asm: with T a compile-time (1,1,1) the gfx950
+        // backend dropped T.xy on the dielectric-reflect path of scatter (ROCm 7.2 clang;
+        // T.xy came out as stale registers while T.z was right).  Keeping T opaque gives the
+        // same code shape as bounces >= 1, which is parity-clean.
+        float tx = 1.f, ty = 1.f, tz = 1.f;
+        asm volatile("" : "+v"(tx), "+v"(ty), "+v"(tz));
+        T = v3(tx, ty, tz);
+        C = v3(0, 0, 0);
+    } else {
+        const float4 r0 = geo[(size_t)slot * 2], r1 = geo[(size_t)slot * 2 + 1], r2 = tc[slot];
+        o = v3(r0.x, r0.y, r0.z);
+        d = v3(r0.w, r1.x, r1.y);
+        T = v3(r1.z, r1.w, r2.x);
+        C = v3(r2.y, r2.z, r2.w);
+    }
+    V3 no = o, nd = d;
+    if (index == -1) {
+        C = C + sky_color(S.env, S.env_w, S.env_h, d) * T;
+        T = v3(0, 0, 0);
+    } else {
+        no = o + closest * d;
+        V3 normal;
+        if (index < S.sphere_count) {
+            const float4 sph = S.spheres[index];
+            normal = (1 / sph.w) * (no - v3(sph.x, sph.y, sph.z));
+        } else {
+            const float4 q2 = S.tris[(size_t)(index - S.sphere_count) * 3 + 2];
+            normal = v3(q2.y, q2.z, q2.w);
+        }
+        scatter(d, normal, load_mat(S.mats + (size_t)S.mat_idx[index] * 3), rng, T, C, nd);
+    }
+    return Shaded{no, nd, T, C, FIRST ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot],
+                  index == -1 ? 0 : (index < S.sphere_count ? 2 : 1)};
+}
+
 // Shading for the live slots (scene.cu:376-485): environment lookup on a miss, otherwise
 // emission + scatter; then the new ray state and its reorder bucket.  One lane per slot.
 // Ray state lives in slot order (the reorder moves it), so every access here is coalesced.  A
@@ -478,60 +539,18 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
     for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
         const int slot = base + threadIdx.x;
         if (slot >= L) continue;
-        // The seed follows the reference's slot (raytracing.cu:89): the position with sort on;
-        // with sort off a ray keeps its original slot, which is its ray id.  At bounce 0 the
-        // reference slot is the ray id (pixel-tile renders: mapped from this tile's slot).
-        const uint32_t ray0 = first_ray<FIRST>(pa.map, (uint32_t)slot);   // bounce 0 only
-        const uint32_t seed_slot = (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
-        Rng rng = pcg_seed(seed_slot * 4137874753u + seed_term);
-        const float2 h = hits[slot];
-        const float closest = h.x;
-        const int index = __float_as_int(h.y);
-        V3 o, d, T, C;
-        if (FIRST) {
-            o = S.cam;
-            d = primary_dir(S, FIRST == 2 ? (int)ray0 : slot, pa);
-            // T is laundered through an empty asm: with T a compile-time (1,1,1) the gfx950
-            // backend dropped T.xy on the dielectric-reflect path of scatter (ROCm 7.2 clang;
-            // T.xy came out as stale registers while T.z was right).  Keeping T opaque gives the
-            // same code shape as bounces >= 1, which is parity-clean.
-            float tx = 1.f, ty = 1.f, tz = 1.f;
-            asm volatile("" : "+v"(tx), "+v"(ty), "+v"(tz));
-            T = v3(tx, ty, tz);
-            C = v3(0, 0, 0);
-        } else {
-            const float4 r0 = geo[(size_t)slot * 2], r1 = geo[(size_t)slot * 2 + 1], r2 = tc[slot];
-            o = v3(r0.x, r0.y, r0.z);
-            d = v3(r0.w, r1.x, r1.y);
-            T = v3(r1.z, r1.w, r2.x);
-            C = v3(r2.y, r2.z, r2.w);
-        }
-        V3 no = o, nd = d;
-        if (index == -1) {
-            miss++;
-            C = C + sky_color(S.env, S.env_w, S.env_h, d) * T;
-            T = v3(0, 0, 0);
-        } else {
-            hit++;
-            no = o + closest * d;
-            V3 normal;
-            if (index < S.sphere_count) {
-                hit_sphere++;
-                const float4 sph = S.spheres[index];
-                normal = (1 / sph.w) * (no - v3(sph.x, sph.y, sph.z));
-            } else {
-                const float4 q2 = S.tris[(size_t)(index - S.sphere_count) * 3 + 2];
-                normal = v3(q2.y, q2.z, q2.w);
-            }
-            scatter(d, normal, load_mat(S.mats + (size_t)S.mat_idx[index] * 3), rng, T, C, nd);
-        }
+        const Shaded sh = shade_one<SORTED, FIRST>(S, pa, slot, geo, tc, rid, hits, seed_term);
+        const V3 no = sh.no, nd = sh.nd, T = sh.T, C = sh.C;
+        miss += sh.kind == 0;
+        hit += sh.kind != 0;
+        hit_sphere += sh.kind == 2;
         const bool dead = is_black(T);
         const float4 tcv = make_float4(T.z, C.x, C.y, C.z);
         if (!dead && !last) {           // a terminated ray's geometry is never read again
             geo[(size_t)slot * 2] = make_float4(no.x, no.y, no.z, nd.x);
             geo[(size_t)slot * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
         }
-        if (dead || last) acc[FIRST ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot]] = tcv;
+        if (dead || last) acc[sh.ray] = tcv;
         else tc[slot] = tcv;
         if (!last) bkt[slot] = (uint8_t)(dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u));
     }
