@@ -160,9 +160,10 @@ __global__ __launch_bounds__(kThreads) void bounds_kernel(const NodeRange *__res
         float scale[3];
         for (int a = 0; a < 3; a++) scale[a] = kBins / (cmax[a] - cmin[a]);   // scene.cu:911
         // Neighbouring triangles mostly share a bin, so per-lane atomics would serialise 64 ways on
-        // one LDS word: the lanes holding the same bin are found by ballot, reduced across the
-        // wave by shuffles, and one lane per (wave, bin) does the atomics.  The loop is
-        // wave-uniform (ballots need every lane).
+        // one LDS word: in the 16-wave (big-node) variant the lanes holding the same bin are found
+        // by ballot, reduced across the wave by shuffles, and one lane per (wave, bin) does the
+        // atomics (lamp root: 5.4 -> ~2 ms).  Small nodes' bins vary more across a wave, and there
+        // the per-lane atomics are cheaper.  The loop is wave-uniform (ballots need every lane).
         for (int i0 = lo + (t & ~63); i0 < hi; i0 += kThreads) {
             const int i = i0 + lane;
             const bool valid = i < hi;
@@ -173,6 +174,16 @@ __global__ __launch_bounds__(kThreads) void bounds_kernel(const NodeRange *__res
             for (int a = 0; a < 3; a++) {
                 if (cmin[a] == cmax[a]) continue;
                 const int b = min(kBins - 1, (int)((cc[a] - cmin[a]) * scale[a]));   // scene.cu:918
+                if (kWaves == 1) {      // one-wave nodes (<= 4096 triangles): plain per-lane atomics
+                    if (valid) {
+                        atomicAdd(&s_wcnt[w][a][b], 1);
+                        for (int q = 0; q < 3; q++) {
+                            atomicMin(&s_wkey[w][a][b][q], kl[q]);
+                            atomicMax(&s_wkey[w][a][b][q + 3], kh[q]);
+                        }
+                    }
+                    continue;
+                }
                 unsigned long long rem = __ballot(valid);
                 while (rem) {
                     const int leader = __ffsll((long long)rem) - 1;
