@@ -43,9 +43,28 @@ constexpr int kBins = 8;              // scene.cu:896
 constexpr int kBig = 1024;              // workgroup per node above kBigMin triangles: 16 waves
 constexpr int kSmall = 64;             // one wave per smaller node
 constexpr int kBigMin = 4096;
+constexpr int kHuge = 32768;           // nodes above this: box and bins reduced over chunks of kChunk
+constexpr int kChunk = 8192;           // triangles by many workgroups, then combined
 
 struct NodeRange {                     // one node of the current level
     int begin, end;
+};
+
+struct Chunk {                         // a huge node's triangle sub-range
+    int lo, hi;
+    int first, n;                      // the node's chunks: [first, first + n)
+    int count;                         // the node's triangle count
+};
+
+struct BoxPartial {                    // a chunk's box (value, index) extremes and centroid range
+    float v[6];
+    int vi[6];
+    float c[6];
+};
+
+struct BinPartial {                    // a chunk's bin counts and bin bound keys
+    int cnt[3][8];
+    int key[3][8][6];
 };
 
 struct NodeOut {                       // per node of the level, written by the kernels
@@ -84,13 +103,28 @@ __device__ __forceinline__ float half_area(const float lo[3], const float hi[3])
 }
 
 // Node box, centroid ranges, bins and the split decision (scene.cu:868-955).
-template <int kThreads>
-__global__ __launch_bounds__(kThreads) void bounds_kernel(const NodeRange *__restrict__ nodes, int depth_left,
+// MODE 0: one workgroup per node does everything.  Huge nodes are spread over workgroups:
+// MODE 1: per chunk, the box/centroid extremes -> pbox;  MODE 2: per chunk, the node's box from
+// its chunks' pbox, then the chunk's bins -> pbin;  MODE 3: per node, box and bins combined from
+// the chunks, then the decision.  (value, index) extremes, integer counts and min/max keys
+// combine in any order, so every mode yields the same NodeOut.
+template <int kThreads, int MODE>
+__global__ __launch_bounds__(kThreads) void bounds_kernel(const NodeRange *__restrict__ nodes,
+                                                          const Chunk *__restrict__ chunks,
+                                                          const int2 *__restrict__ huge, int depth_left,
                                                           const float4 *__restrict__ blo, const float4 *__restrict__ bhi,
-                                                          const float4 *__restrict__ cen, NodeOut *__restrict__ out) {
+                                                          const float4 *__restrict__ cen, NodeOut *__restrict__ out,
+                                                          BoxPartial *__restrict__ pbox, BinPartial *__restrict__ pbin) {
     constexpr int kWaves = kThreads / 64;
-    const NodeRange nr = nodes[blockIdx.x];
-    const int lo = nr.begin, hi = nr.end, count = hi - lo;
+    int lo, hi, count, first = 0, nch = 0;
+    if (MODE == 1 || MODE == 2) {
+        const Chunk ch = chunks[blockIdx.x];
+        lo = ch.lo; hi = ch.hi; count = ch.count; first = ch.first; nch = ch.n;
+    } else {
+        const NodeRange nr = nodes[blockIdx.x];
+        lo = nr.begin; hi = nr.end; count = hi - lo;
+        if (MODE == 3) { first = huge[blockIdx.x].x; nch = huge[blockIdx.x].y; }
+    }
     const int t = threadIdx.x;
     __shared__ float s_v[6][kWaves];
     __shared__ int s_i[6][kWaves];
@@ -104,6 +138,15 @@ __global__ __launch_bounds__(kThreads) void bounds_kernel(const NodeRange *__res
     float v[6] = {1e30f, 1e30f, 1e30f, -1e30f, -1e30f, -1e30f};
     int vi[6] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
     float c[6] = {1e30f, 1e30f, 1e30f, -1e30f, -1e30f, -1e30f};
+    if (MODE >= 2) {                    // combine the node's chunk extremes (every thread)
+        for (int q = first; q < first + nch; q++) {
+            const BoxPartial &pb = pbox[q];
+            for (int k = 0; k < 6; k++) {
+                if (k < 3) arg_min(v[k], vi[k], pb.v[k], pb.vi[k]); else arg_max(v[k], vi[k], pb.v[k], pb.vi[k]);
+                c[k] = k < 3 ? ref_min(c[k], pb.c[k]) : ref_max(c[k], pb.c[k]);
+            }
+        }
+    } else {
 #pragma unroll 4
     for (int i = lo + t; i < hi; i += kThreads) {
         const float4 l = blo[i], h = bhi[i], ce = cen[i];
@@ -136,6 +179,14 @@ __global__ __launch_bounds__(kThreads) void bounds_kernel(const NodeRange *__res
         v[k] = a;
         c[k] = cc;
     }
+    }
+    if (MODE == 1) {
+        if (t == 0) {
+            BoxPartial &pb = pbox[blockIdx.x];
+            for (int k = 0; k < 6; k++) { pb.v[k] = v[k]; pb.vi[k] = vi[k]; pb.c[k] = c[k]; }
+        }
+        return;
+    }
     // The reference starts from the fresh node's (1e30, -1e30) box: a range reduced to those
     // (empty, or only NaN-free sentinels) leaves them as they are.
     float box_lo[3], box_hi[3], cmin[3], cmax[3];
@@ -146,7 +197,23 @@ __global__ __launch_bounds__(kThreads) void bounds_kernel(const NodeRange *__res
         cmax[k] = ref_max(-1e30f, c[k + 3]);
     }
     const bool may_split = count > 4 && depth_left > 0;
-    if (may_split) {
+    if (MODE == 2 && !may_split) return;
+    if (may_split && MODE == 3) {        // the chunks' bins
+        for (int k = t; k < 3 * kBins; k += kThreads) {
+            const int a = k / kBins, b = k % kBins;
+            int cnt = 0, key[6] = {fkey(1e30f), fkey(1e30f), fkey(1e30f), fkey(-1e30f), fkey(-1e30f), fkey(-1e30f)};
+            for (int q = first; q < first + nch; q++) {
+                cnt += pbin[q].cnt[a][b];
+                for (int z = 0; z < 3; z++) {
+                    key[z] = min(key[z], pbin[q].key[a][b][z]);
+                    key[z + 3] = max(key[z + 3], pbin[q].key[a][b][z + 3]);
+                }
+            }
+            s_cnt[a][b] = cnt;
+            for (int z = 0; z < 6; z++) s_key[a][b][z] = key[z];
+        }
+        __syncthreads();
+    } else if (may_split) {
         // Bins per wave in LDS (integer atomics on keys that order like the floats; only 64 lanes
         // contend for a wave's bins), then combined over the waves.
         const int w = t >> 6, lane = t & 63;
@@ -228,6 +295,14 @@ __global__ __launch_bounds__(kThreads) void bounds_kernel(const NodeRange *__res
             for (int q = 0; q < 6; q++) s_key[a][b][q] = key[q];
         }
         __syncthreads();
+        if (MODE == 2) {
+            for (int k = t; k < 3 * kBins; k += kThreads) {
+                const int a = k / kBins, b = k % kBins;
+                pbin[blockIdx.x].cnt[a][b] = s_cnt[a][b];
+                for (int q = 0; q < 6; q++) pbin[blockIdx.x].key[a][b][q] = s_key[a][b][q];
+            }
+            return;
+        }
     }
     if (t != 0) return;
     NodeOut o;
@@ -502,12 +577,23 @@ int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vecto
     Buf<uint8_t> side;
     Buf<NodeRange> d_nodes;
     Buf<NodeOut> d_out;
+    Buf<Chunk> d_chunks;
+    Buf<int2> d_huge;
+    Buf<BoxPartial> pbox;
+    Buf<BinPartial> pbin;
     const size_t m = std::max(n, 1);
     BCHK(blo.alloc(m)); BCHK(bhi.alloc(m)); BCHK(cen.alloc(m));
     BCHK(t_blo.alloc(m)); BCHK(t_bhi.alloc(m)); BCHK(t_cen.alloc(m));
     BCHK(idx.alloc(m)); BCHK(t_idx.alloc(m)); BCHK(xk.alloc(m)); BCHK(rk.alloc(m)); BCHK(side.alloc(m));
     // a level holds at most n / 1 nodes (ranges are disjoint and non-empty below the root)
     BCHK(d_nodes.alloc(m)); BCHK(d_out.alloc(m));
+    // chunks of the huge nodes of a level: disjoint ranges of > kHuge triangles, so fewer than
+    // n / kChunk + n / kHuge of them
+    const size_t max_chunks = (size_t)n / kChunk + (size_t)n / kHuge + 1;
+    BCHK(d_chunks.alloc(max_chunks)); BCHK(d_huge.alloc(max_chunks));
+    BCHK(pbox.alloc(max_chunks)); BCHK(pbin.alloc(max_chunks));
+    std::vector<Chunk> h_chunks;
+    std::vector<int2> h_huge;
     // the per-thread default stream: the build is synchronous, and a stream costs ~3.6 ms to create
     hipStream_t s = hipStreamPerThread;
     BCHK(hipMemcpyAsync(blo.p, h_lo.data(), m * sizeof(float4), hipMemcpyHostToDevice, s));
@@ -527,26 +613,51 @@ int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vecto
     for (int depth = 0; !level.empty(); depth++) {
         const auto t_level = clk::now();
         const int cnt = (int)level.size();
-        // big nodes first (a 16-wave workgroup each), then the rest (one wave each)
-        std::stable_partition(level.begin(), level.end(),
-                              [&](int x) { return tree[x].end - tree[x].begin > kBigMin; });
-        int nbig = 0;
+        // huge nodes first (box and bins over many workgroups), then big ones (a 16-wave
+        // workgroup each), then the rest (one wave each)
+        auto len_of = [&](int x) { return tree[x].end - tree[x].begin; };
+        std::stable_partition(level.begin(), level.end(), [&](int x) { return len_of(x) > kBigMin; });
+        std::stable_partition(level.begin(), level.end(), [&](int x) { return len_of(x) > kHuge; });
+        int nbig = 0, nhuge = 0;
         h_ranges.resize(cnt);
+        h_chunks.clear();
+        h_huge.clear();
         for (int k = 0; k < cnt; k++) {
             h_ranges[k] = {tree[level[k]].begin, tree[level[k]].end};
-            nbig += h_ranges[k].end - h_ranges[k].begin > kBigMin;
+            const int len = h_ranges[k].end - h_ranges[k].begin;
+            nbig += len > kBigMin;
+            if (len > kHuge) {
+                nhuge++;
+                const int first = (int)h_chunks.size(), nch = (len + kChunk - 1) / kChunk;
+                for (int j = 0; j < nch; j++)
+                    h_chunks.push_back(Chunk{h_ranges[k].begin + j * kChunk,
+                                             std::min(h_ranges[k].end, h_ranges[k].begin + (j + 1) * kChunk), first, nch,
+                                             len});
+                h_huge.push_back(make_int2(first, nch));
+            }
         }
         BCHK(hipMemcpyAsync(d_nodes.p, h_ranges.data(), cnt * sizeof(NodeRange), hipMemcpyHostToDevice, s));
         const int left_depth = max_depth - depth;
-        if (nbig) {
-            hipLaunchKernelGGL(bounds_kernel<kBig>, dim3(nbig), dim3(kBig), 0, s, d_nodes.p, left_depth, blo.p, bhi.p,
-                               cen.p, d_out.p);
+        if (nhuge) {
+            const int nch = (int)h_chunks.size();
+            BCHK(hipMemcpyAsync(d_chunks.p, h_chunks.data(), nch * sizeof(Chunk), hipMemcpyHostToDevice, s));
+            BCHK(hipMemcpyAsync(d_huge.p, h_huge.data(), nhuge * sizeof(int2), hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL((bounds_kernel<kBig, 1>), dim3(nch), dim3(kBig), 0, s, d_nodes.p, d_chunks.p, d_huge.p,
+                               left_depth, blo.p, bhi.p, cen.p, d_out.p, pbox.p, pbin.p);
+            hipLaunchKernelGGL((bounds_kernel<kBig, 2>), dim3(nch), dim3(kBig), 0, s, d_nodes.p, d_chunks.p, d_huge.p,
+                               left_depth, blo.p, bhi.p, cen.p, d_out.p, pbox.p, pbin.p);
+            hipLaunchKernelGGL((bounds_kernel<kSmall, 3>), dim3(nhuge), dim3(kSmall), 0, s, d_nodes.p, d_chunks.p,
+                               d_huge.p, left_depth, blo.p, bhi.p, cen.p, d_out.p, pbox.p, pbin.p);
+        }
+        if (nbig > nhuge)
+            hipLaunchKernelGGL((bounds_kernel<kBig, 0>), dim3(nbig - nhuge), dim3(kBig), 0, s, d_nodes.p + nhuge,
+                               d_chunks.p, d_huge.p, left_depth, blo.p, bhi.p, cen.p, d_out.p + nhuge, pbox.p, pbin.p);
+        if (nbig)
             hipLaunchKernelGGL(partition_kernel<kBig>, dim3(nbig), dim3(kBig), 0, s, d_nodes.p, d_out.p, idx.p, blo.p,
                                bhi.p, cen.p, t_idx.p, t_blo.p, t_bhi.p, t_cen.p, xk.p, rk.p, side.p);
-        }
         if (cnt > nbig) {
-            hipLaunchKernelGGL(bounds_kernel<kSmall>, dim3(cnt - nbig), dim3(kSmall), 0, s, d_nodes.p + nbig,
-                               left_depth, blo.p, bhi.p, cen.p, d_out.p + nbig);
+            hipLaunchKernelGGL((bounds_kernel<kSmall, 0>), dim3(cnt - nbig), dim3(kSmall), 0, s, d_nodes.p + nbig,
+                               d_chunks.p, d_huge.p, left_depth, blo.p, bhi.p, cen.p, d_out.p + nbig, pbox.p, pbin.p);
             hipLaunchKernelGGL(partition_kernel<kSmall>, dim3(cnt - nbig), dim3(kSmall), 0, s, d_nodes.p + nbig,
                                d_out.p + nbig, idx.p, blo.p, bhi.p, cen.p, t_idx.p, t_blo.p, t_bhi.p, t_cen.p, xk.p, rk.p, side.p);
         }
