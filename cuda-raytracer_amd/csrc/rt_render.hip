@@ -60,12 +60,21 @@ namespace {
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 constexpr int kStackLds = RT_STACK_LDS; // stack entries per lane kept in LDS (deeper: global)
 constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138)
-constexpr int kSortItems = 16;        // sort tile = kBlock * kSortItems slots
+#ifndef RT_SORT_ITEMS
+#define RT_SORT_ITEMS 16
+#endif
+#ifndef RT_CHUNK_MIN
+#define RT_CHUNK_MIN 64
+#endif
+#ifndef RT_SHADE_BPC
+#define RT_SHADE_BPC 8
+#endif
+constexpr int kSortItems = RT_SORT_ITEMS;   // sort tile = kBlock * kSortItems slots
 constexpr int kSortTile = kBlock * kSortItems;
 constexpr int kBuckets = 65;
 constexpr int kCtrSlots = 64;       // striped copies of the work counters
 constexpr int kChunkMax = RT_CHUNK_MAX; // slots a wave takes from the trace queue per atomic...
-constexpr int kChunkMin = 64;        // ...shrunk so that every wave gets ~4 chunks when few rays live
+constexpr int kChunkMin = RT_CHUNK_MIN; // ...shrunk so that every wave gets ~4 chunks when few rays live
 constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are idle
 constexpr int kRefillFirst = RT_REFILL_FIRST;   // same at bounce 0: a whole wave of consecutive primary rays
                                                 // (~3 pixels) starts together and stays in lockstep
@@ -1097,7 +1106,7 @@ struct rt_renderer {
         const int grid = blocks_for(n);
         const int tiles = (n + kSortTile - 1) / kSortTile;
         const int tgrid = std::min(grid, trace_blocks);
-        const int sgrid = std::min(grid, cus * 8);
+        const int sgrid = std::min(grid, cus * RT_SHADE_BPC);
         // tile-stride reorder kernels on at most 8 blocks per CU: in the tail bounces a block per
         // possible tile dispatched ~10^4 empty workgroups per launch (A/B: +0.3-0.5 %)
         const int sort_grid = std::min(tiles, RT_SORT_GRID > 0 ? RT_SORT_GRID : cus * 8);
