@@ -43,14 +43,21 @@ constexpr int kBins = 8;              // scene.cu:896
 constexpr int kBig = 1024;              // workgroup per node above kBigMin triangles: 16 waves
 constexpr int kSmall = 64;             // one wave per smaller node
 constexpr int kBigMin = 4096;
-constexpr int kHuge = 32768;           // nodes above this: box and bins reduced over chunks of kChunk
-constexpr int kChunk = 8192;           // triangles by many workgroups, then combined
+#ifndef RT_BVH_HUGE
+#define RT_BVH_HUGE 32768
+#endif
+#ifndef RT_BVH_CHUNK
+#define RT_BVH_CHUNK 8192
+#endif
+constexpr int kHuge = RT_BVH_HUGE;     // nodes above this: box, bins and partition over chunks of kChunk
+constexpr int kChunk = RT_BVH_CHUNK;   // triangles, one workgroup each, then combined
 
 struct NodeRange {                     // one node of the current level
     int begin, end;
 };
 
 struct Chunk {                         // a huge node's triangle sub-range
+    int node;                          // the node's index in the level (huge nodes come first)
     int lo, hi;
     int first, n;                      // the node's chunks: [first, first + n)
     int count;                         // the node's triangle count
@@ -511,6 +518,151 @@ __global__ __launch_bounds__(kThreads) void partition_kernel(const NodeRange *__
     if (t == 0) out[blockIdx.x].left = L;
 }
 
+
+// The closed-form partition of a huge node over its chunks (one workgroup per chunk; the same
+// moves as partition_kernel, with the ranks made global by the chunks' counts):
+//   P1 side bytes and lefts per chunk; P2 front rights / back lefts / back rights per chunk
+//   (front = positions [0, a), back = [a, n)); P3 X[k] for the front rights, R[j] for the back
+//   lefts, back rights to their places; P4 back lefts to X[j], front rights to
+//   n-1-(k + R[k-1]), front lefts in place; P5 the node's range back from tmp.
+// Back ranks count in the reference's examination order from the end (descending positions).
+struct PartCounts { int l, fr, bl, br; };
+
+__device__ __forceinline__ void huge_node_split(const Chunk &ch, const PartCounts *cnt, const uint8_t *S, int n,
+                                                int &L, int &a) {
+    L = 0;
+    for (int q = ch.first; q < ch.first + ch.n; q++) L += cnt[q].l;
+    a = (L == n || S[L]) ? L : L + 1;
+}
+
+template <int kThreads, int PHASE>
+__global__ __launch_bounds__(kThreads) void partition_huge_kernel(const NodeRange *__restrict__ nodes,
+                                                                  const Chunk *__restrict__ chunks,
+                                                                  NodeOut *__restrict__ out, uint32_t *__restrict__ idx,
+                                                                  float4 *__restrict__ blo, float4 *__restrict__ bhi,
+                                                                  float4 *__restrict__ cen, uint32_t *__restrict__ t_idx,
+                                                                  float4 *__restrict__ t_blo, float4 *__restrict__ t_bhi,
+                                                                  float4 *__restrict__ t_cen, int *__restrict__ xk,
+                                                                  int *__restrict__ rk, uint8_t *__restrict__ side,
+                                                                  PartCounts *__restrict__ cnt) {
+    const Chunk ch = chunks[blockIdx.x];
+    const NodeOut no = out[ch.node];
+    if (no.axis < 0) return;
+    const int base = nodes[ch.node].begin, n = ch.count;
+    const int c0 = ch.lo - base, c1 = ch.hi - base;         // this chunk's positions in the node
+    const int t = threadIdx.x;
+    constexpr int kWaves = kThreads / 64, kTile = kThreads * kPer;
+    __shared__ int s_scan[kWaves];
+    uint8_t *S = side + base;
+    int *X = xk + base, *R = rk + base;
+    auto move = [&](int from, int to) {
+        t_idx[base + to] = idx[base + from];
+        t_blo[base + to] = blo[base + from];
+        t_bhi[base + to] = bhi[base + from];
+        t_cen[base + to] = cen[base + from];
+    };
+    if (PHASE == 1) {
+        int c = 0;
+        for (int p = c0 + t; p < c1; p += kThreads) {
+            const float4 ce = cen[base + p];
+            const float v = no.axis == 0 ? ce.x : (no.axis == 1 ? ce.y : ce.z);
+            const bool l = v < no.pos;
+            S[p] = l ? 1 : 0;
+            c += l;
+        }
+        int tot;
+        (void)block_scan<kWaves>(c, &tot, s_scan);
+        if (t == 0) cnt[blockIdx.x].l = tot;
+        return;
+    }
+    if (PHASE == 5) {
+        for (int p = c0 + t; p < c1; p += kThreads) {
+            idx[base + p] = t_idx[base + p];
+            blo[base + p] = t_blo[base + p];
+            bhi[base + p] = t_bhi[base + p];
+            cen[base + p] = t_cen[base + p];
+        }
+        if (blockIdx.x == (unsigned)ch.first && t == 0) {
+            int L, a;
+            huge_node_split(ch, cnt, S, n, L, a);
+            out[ch.node].left = L;
+        }
+        return;
+    }
+    int L, a;
+    huge_node_split(ch, cnt, S, n, L, a);
+    const int f0 = c0, f1 = min(c1, a);                      // front part of the chunk: [f0, f1)
+    const int b0 = max(c0, a), b1 = c1;                      // back part: [b0, b1), walked b1-1 down to b0
+    if (PHASE == 2) {
+        int fr = 0, bl = 0, br = 0;
+        for (int p = f0 + t; p < f1; p += kThreads) fr += S[p] ? 0 : 1;
+        for (int p = b0 + t; p < b1; p += kThreads) { bl += S[p]; br += S[p] ? 0 : 1; }
+        int tfr, tbl, tbr;
+        (void)block_scan<kWaves>(fr, &tfr, s_scan);
+        (void)block_scan<kWaves>(bl, &tbl, s_scan);
+        (void)block_scan<kWaves>(br, &tbr, s_scan);
+        if (t == 0) { cnt[blockIdx.x].fr = tfr; cnt[blockIdx.x].bl = tbl; cnt[blockIdx.x].br = tbr; }
+        return;
+    }
+    // global rank offsets: front rights of earlier chunks; back lefts / rights of later chunks
+    int fr_before = 0, bl_after = 0, br_after = 0;
+    for (int q = ch.first; q < (int)blockIdx.x; q++) fr_before += cnt[q].fr;
+    for (int q = blockIdx.x + 1; q < ch.first + ch.n; q++) { bl_after += cnt[q].bl; br_after += cnt[q].br; }
+    // back part, descending positions (the reference's order from the end)
+    const int nb = b1 - b0;
+    int run_l = bl_after, run_r = br_after;
+    for (int y0 = 0; y0 < nb; y0 += kTile) {
+        uint8_t f[kPer];                    // 0 none, 1 left, 2 right
+        int cl = 0, cr = 0;
+        for (int j = 0; j < kPer; j++) {
+            const int y = y0 + t * kPer + j;
+            f[j] = y < nb ? (S[b1 - 1 - y] ? 1 : 2) : 0;
+            cl += f[j] == 1;
+            cr += f[j] == 2;
+        }
+        int tot;
+        const int packed = block_scan<kWaves>(cl | (cr << 16), &tot, s_scan);
+        int kl = run_l + (packed & 0xffff), kr = run_r + (packed >> 16);
+        for (int j = 0; j < kPer; j++) {
+            const int p = b1 - 1 - (y0 + t * kPer + j);
+            if (f[j] == 1) {
+                if (PHASE == 3) R[kl] = kr;
+                else move(p, X[kl]);
+                kl++;
+            } else if (f[j] == 2) {
+                if (PHASE == 3) move(p, n - 1 - (kl + 1 + kr));
+                kr++;
+            }
+        }
+        run_l += tot & 0xffff;
+        run_r += tot >> 16;
+    }
+    // front part, ascending positions
+    int run = fr_before;
+    for (int p0 = f0; p0 < f1; p0 += kTile) {
+        uint8_t f[kPer];                    // 0 none, 1 left, 2 right
+        int c = 0;
+        for (int j = 0; j < kPer; j++) {
+            const int p = p0 + t * kPer + j;
+            f[j] = p < f1 ? (S[p] ? 1 : 2) : 0;
+            c += f[j] == 2;
+        }
+        int tot;
+        int k = run + block_scan<kWaves>(c, &tot, s_scan);
+        for (int j = 0; j < kPer; j++) {
+            const int p = p0 + t * kPer + j;
+            if (f[j] == 2) {
+                if (PHASE == 3) X[k] = p;
+                else move(p, n - 1 - (k + (k >= 1 ? R[k - 1] : 0)));
+                k++;
+            } else if (f[j] == 1 && PHASE == 4) {
+                move(p, p);
+            }
+        }
+        run += tot;
+    }
+}
+
 #define BCHK(call)                                                                                 \
     do {                                                                                           \
         const hipError_t e_ = (call);                                                              \
@@ -581,6 +733,7 @@ int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vecto
     Buf<int2> d_huge;
     Buf<BoxPartial> pbox;
     Buf<BinPartial> pbin;
+    Buf<PartCounts> pcnt;
     const size_t m = std::max(n, 1);
     BCHK(blo.alloc(m)); BCHK(bhi.alloc(m)); BCHK(cen.alloc(m));
     BCHK(t_blo.alloc(m)); BCHK(t_bhi.alloc(m)); BCHK(t_cen.alloc(m));
@@ -591,7 +744,7 @@ int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vecto
     // n / kChunk + n / kHuge of them
     const size_t max_chunks = (size_t)n / kChunk + (size_t)n / kHuge + 1;
     BCHK(d_chunks.alloc(max_chunks)); BCHK(d_huge.alloc(max_chunks));
-    BCHK(pbox.alloc(max_chunks)); BCHK(pbin.alloc(max_chunks));
+    BCHK(pbox.alloc(max_chunks)); BCHK(pbin.alloc(max_chunks)); BCHK(pcnt.alloc(max_chunks));
     std::vector<Chunk> h_chunks;
     std::vector<int2> h_huge;
     // the per-thread default stream: the build is synchronous, and a stream costs ~3.6 ms to create
@@ -630,7 +783,7 @@ int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vecto
                 nhuge++;
                 const int first = (int)h_chunks.size(), nch = (len + kChunk - 1) / kChunk;
                 for (int j = 0; j < nch; j++)
-                    h_chunks.push_back(Chunk{h_ranges[k].begin + j * kChunk,
+                    h_chunks.push_back(Chunk{k, h_ranges[k].begin + j * kChunk,
                                              std::min(h_ranges[k].end, h_ranges[k].begin + (j + 1) * kChunk), first, nch,
                                              len});
                 h_huge.push_back(make_int2(first, nch));
@@ -652,9 +805,19 @@ int gpu_build_bvh(std::vector<rt_triangle> &tris, uint16_t *tri_mats, std::vecto
         if (nbig > nhuge)
             hipLaunchKernelGGL((bounds_kernel<kBig, 0>), dim3(nbig - nhuge), dim3(kBig), 0, s, d_nodes.p + nhuge,
                                d_chunks.p, d_huge.p, left_depth, blo.p, bhi.p, cen.p, d_out.p + nhuge, pbox.p, pbin.p);
-        if (nbig)
-            hipLaunchKernelGGL(partition_kernel<kBig>, dim3(nbig), dim3(kBig), 0, s, d_nodes.p, d_out.p, idx.p, blo.p,
-                               bhi.p, cen.p, t_idx.p, t_blo.p, t_bhi.p, t_cen.p, xk.p, rk.p, side.p);
+        if (nhuge) {
+            const int nch = (int)h_chunks.size();
+#define RT_PART_HUGE(PH)                                                                                         \
+    hipLaunchKernelGGL((partition_huge_kernel<kBig, PH>), dim3(nch), dim3(kBig), 0, s, d_nodes.p, d_chunks.p,     \
+                       d_out.p, idx.p, blo.p, bhi.p, cen.p, t_idx.p, t_blo.p, t_bhi.p, t_cen.p, xk.p, rk.p, side.p, \
+                       pcnt.p)
+            RT_PART_HUGE(1); RT_PART_HUGE(2); RT_PART_HUGE(3); RT_PART_HUGE(4); RT_PART_HUGE(5);
+#undef RT_PART_HUGE
+        }
+        if (nbig > nhuge)
+            hipLaunchKernelGGL(partition_kernel<kBig>, dim3(nbig - nhuge), dim3(kBig), 0, s, d_nodes.p + nhuge,
+                               d_out.p + nhuge, idx.p, blo.p, bhi.p, cen.p, t_idx.p, t_blo.p, t_bhi.p, t_cen.p, xk.p,
+                               rk.p, side.p);
         if (cnt > nbig) {
             hipLaunchKernelGGL((bounds_kernel<kSmall, 0>), dim3(cnt - nbig), dim3(kSmall), 0, s, d_nodes.p + nbig,
                                d_chunks.p, d_huge.p, left_depth, blo.p, bhi.p, cen.p, d_out.p + nbig, pbox.p, pbin.p);

@@ -46,7 +46,7 @@ def test_gpu_build_edge_scenes(gpu, tmp_path):
         _same(p)
 
 
-@pytest.mark.parametrize("seed,n", [(1, 3000), (2, 20000), (3, 777)])
+@pytest.mark.parametrize("seed,n", [(1, 3000), (2, 20000), (3, 777), (4, 90000)])   # 90000: chunked huge nodes
 def test_gpu_build_random_soup_with_ties(gpu, tmp_path, seed, n):
     rng = np.random.default_rng(seed)
     vals = np.array([-2.0, -1.0, -0.0, 0.0, 0.5, 1.0, 3.0], np.float64)
