@@ -237,6 +237,9 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #ifndef RT_TRACE_WPE
 #define RT_TRACE_WPE 8
 #endif
+#ifndef RT_FUSED_MAX_TRIS
+#define RT_FUSED_MAX_TRIS 4096        // fused reorder for scenes up to this many triangles (see enqueue_pass)
+#endif
 #ifndef RT_SORT_GRID
 #define RT_SORT_GRID 0                // cap on the reorder's hist/scatter grid (0: 8 blocks per CU)
 #endif
@@ -536,7 +539,7 @@ __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &p
 // Ray state lives in slot order (the reorder moves it), so every access here is coalesced.  A
 // ray's radiance goes to acc[ray id] (pixel-major, what accumulation reads) when it terminates
 // or after the last bounce.
-template <bool SORTED, bool COUNT, int FIRST>
+template <bool SORTED, bool COUNT, int FIRST, bool FUSED>
 __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
                                                        float4 *__restrict__ tc, const uint32_t *__restrict__ rid,
                                                        float4 *__restrict__ acc, uint8_t *__restrict__ bkt,
@@ -555,12 +558,12 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
         hit_sphere += sh.kind == 2;
         const bool dead = is_black(T);
         const float4 tcv = make_float4(T.z, C.x, C.y, C.z);
-        if (!dead && !last) {           // a terminated ray's geometry is never read again
+        if (!FUSED && !dead && !last) {     // a terminated ray's geometry is never read again
             geo[(size_t)slot * 2] = make_float4(no.x, no.y, no.z, nd.x);
             geo[(size_t)slot * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
         }
         if (dead || last) acc[sh.ray] = tcv;
-        else tc[slot] = tcv;
+        else if (!FUSED) tc[slot] = tcv;   // FUSED: the reorder replays the shading instead
         if (!last) bkt[slot] = (uint8_t)(dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u));
     }
     if (COUNT) {
@@ -722,6 +725,68 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
         }
         __syncthreads();
     }
+    }
+}
+
+// Fused reorder (shade_kernel<..., FUSED>): the shade kernel has written only the buckets (and the radiance of
+// terminated rays); this replays the live rays' shading from the same inputs (shade_one is
+// deterministic) and writes the new state straight to its sorted slot, saving the shade
+// kernel's 48-B state write and the plain scatter's 48-B read per live ray.
+template <bool SORTED, int FIRST>
+__global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, PassArgs pa,
+                                                                    const uint8_t *__restrict__ bkt_in,
+                                                                    const float4 *__restrict__ geo_in,
+                                                                    const float4 *__restrict__ tc_in,
+                                                                    const uint32_t *__restrict__ rid_in,
+                                                                    const float2 *__restrict__ hits, uint32_t seed_term,
+                                                                    const uint32_t *__restrict__ live_count, int tiles,
+                                                                    const uint32_t *__restrict__ offsets,
+                                                                    const uint32_t *__restrict__ totals,
+                                                                    float4 *__restrict__ geo_out,
+                                                                    float4 *__restrict__ tc_out,
+                                                                    uint32_t *__restrict__ rid_out) {
+    const int n = (int)*live_count;
+    __shared__ uint32_t run[kBuckets];
+    __shared__ uint32_t wcount[kBlock / 64][kBuckets];
+    for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int b = 0; b < kBuckets; b++) {
+                run[b] = acc + offsets[(size_t)b * tiles + tile];
+                acc += totals[b];
+            }
+        }
+        for (int k = threadIdx.x; k < (kBlock / 64) * kBuckets; k += kBlock) (&wcount[0][0])[k] = 0;
+        __syncthreads();
+        const int wave = threadIdx.x >> 6;
+        const int base = tile * kSortTile;
+        for (int r = 0; r < kSortItems; r++) {
+            const int item = base + r * kBlock + threadIdx.x;
+            const bool valid = item < n;
+            const uint32_t b = valid ? bkt_in[item] : 0u;
+            const bool move = valid && b != kDead;
+            Shaded sh{};
+            if (move) sh = shade_one<SORTED, FIRST>(S, pa, item, geo_in, tc_in, rid_in, hits, seed_term);
+            const unsigned long long peers = match_bucket(b, valid);
+            const uint32_t rank = rank_below(peers);
+            if (valid && rank == 0) wcount[wave][b] = (uint32_t)__popcll(peers);
+            __syncthreads();
+            if (move) {
+                uint32_t pos = run[b] + rank;
+                for (int k = 0; k < wave; k++) pos += wcount[k][b];
+                geo_out[(size_t)pos * 2] = make_float4(sh.no.x, sh.no.y, sh.no.z, sh.nd.x);
+                geo_out[(size_t)pos * 2 + 1] = make_float4(sh.nd.y, sh.nd.z, sh.T.x, sh.T.y);
+                tc_out[pos] = make_float4(sh.T.z, sh.C.x, sh.C.y, sh.C.z);
+                rid_out[pos] = sh.ray;
+            }
+            __syncthreads();
+            if (threadIdx.x < kBuckets) {
+                uint32_t s = 0;
+                for (int k = 0; k < kBlock / 64; k++) { s += wcount[k][threadIdx.x]; wcount[k][threadIdx.x] = 0; }
+                run[threadIdx.x] += s;
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -905,6 +970,12 @@ struct rt_renderer {
     // per-bounce HIP events for rt_stats.process_ms / sort_ms (rt_renderer_set_event_timing): four
     // marker packets per bounce in every pass's stream; off, a frame runs ~2 % faster
     bool pass_events = true;
+    // Fused reorder: shade writes only buckets and the scatter replays the shading (no 48-B state
+    // round trip per live ray).  It pays where traversal is cheap and the bounce is HBM-streaming
+    // bound (spheres: 3.82 -> 3.52 ms/pass); with a big BVH the replay costs more than the
+    // traffic it saves (teapot 7.73 -> 7.79).  On for scenes of <= RT_FUSED_MAX_TRIS triangles;
+    // RTAMD_FUSED=0/1 overrides.
+    bool fused = false;
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
     DevBuf<float4> spheres, tris, mats, nodes;
@@ -943,6 +1014,8 @@ struct rt_renderer {
         tile_count = std::max(1, o->tile_count);
         tile_index = o->tile_index;
         tile_rows = o->tile_rows > 0 ? o->tile_rows : 8;
+        fused = sc->triangle_count <= RT_FUSED_MAX_TRIS;
+        if (const char *f = std::getenv("RTAMD_FUSED")) fused = std::atoi(f) != 0;
         if (tile_index < 0 || tile_index >= tile_count)
             return rtamd::fail(RT_E_INVALID, "tile_index outside [0, tile_count)");
         if (tile_count > 1 && sort)
@@ -1144,9 +1217,14 @@ struct rt_renderer {
     do {                                                                                                         \
         hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,        \
                            c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                                   \
-        hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST>), dim3(sgrid), dim3(kBlock), 0, st, ds, pa,        \
-                           c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p, seed_term,   \
-                           (int)last, ctr.p);                                                                    \
+        if (fused)                                                                                               \
+            hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
+                               pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
+                               seed_term, (int)last, ctr.p);                                                     \
+        else                                                                                                     \
+            hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, false>), dim3(sgrid), dim3(kBlock), 0, st, ds,\
+                               pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
+                               seed_term, (int)last, ctr.p);                                                     \
     } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
     do {                                                                                                         \
@@ -1176,7 +1254,18 @@ struct rt_renderer {
                                    c.sort_counts.p);
                 hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, lv, tiles,
                                    c.sort_offsets.p, c.sort_totals.p, c.live.p + b + 1);
-                if (b == 0 && tiled())
+                if (fused) {
+#define RT_FSC(SO, FI)                                                                                           \
+    hipLaunchKernelGGL((sort_scatter_shade_kernel<SO, FI>), dim3(sort_grid), dim3(kBlock), 0, st, ds, pa, c.bkt.p, \
+                       c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.hits.p, seed_term, lv, tiles, c.sort_offsets.p,  \
+                       c.sort_totals.p, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p)
+                    if (sort) {
+                        if (b == 0) RT_FSC(true, 1); else RT_FSC(true, 0);
+                    } else {
+                        if (b == 0 && tiled()) RT_FSC(false, 2); else if (b == 0) RT_FSC(false, 1); else RT_FSC(false, 0);
+                    }
+#undef RT_FSC
+                } else if (b == 0 && tiled())
                     hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
                                        c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
                                        c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);

@@ -147,3 +147,18 @@ def test_run_host_pass_sums(gpu):
     assert np.array_equal(sums[0], want[0])
     assert np.array_equal(sums[1], osc.pass_sums(sort=True, pass_begin=3, pass_count=1)[0])
     r.close()
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("scene,image,sort", [("teapot", (96, 54, 20, 16), True), ("cornell_plus", (48, 48, 20, 8), False),
+                                              ("spheres", (64, 48, 20, 8), True)])
+def test_fused_and_plain_reorder_bitexact(gpu, monkeypatch, scene, image, sort, fused):
+    # both reorder variants (shade writes the state and the scatter moves it, or the scatter replays
+    # the shading; the renderer picks by scene size, RTAMD_FUSED forces one) against the oracle
+    monkeypatch.setenv("RTAMD_FUSED", fused)
+    osc, psc = _pair(scene, image)
+    ofb, ost = osc.render(sort=sort)
+    gfb, gst = R.render(psc, sort=sort, counters=True)
+    assert np.array_equal(gfb, ofb), _diff(gfb, ofb)
+    assert gst["live_segments"] == ost["live_segments"]
+    assert gst["hits"] == ost["hits_triangle"] + ost["hits_sphere"] and gst["misses"] == ost["misses"]
