@@ -481,7 +481,9 @@ struct Shaded {
     uint32_t ray;
     int kind;
 };
-template <bool SORTED, int FIRST>
+// INLINE (scenes without triangles): the closest hit is the sphere loop (scene.cu:338-372),
+// computed here instead of read from the trace kernel's output.
+template <bool SORTED, int FIRST, bool INLINE = false>
 __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &pa, int slot,
                                             const float4 *__restrict__ geo, const float4 *__restrict__ tc,
                                             const uint32_t *__restrict__ rid, const float2 *__restrict__ hits,
@@ -492,9 +494,13 @@ __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &p
     const uint32_t ray0 = first_ray<FIRST>(pa.map, (uint32_t)slot);   // bounce 0 only
     const uint32_t seed_slot = (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
     Rng rng = pcg_seed(seed_slot * 4137874753u + seed_term);
-    const float2 h = hits[slot];
-    const float closest = h.x;
-    const int index = __float_as_int(h.y);
+    float closest;
+    int index;
+    if (!INLINE) {
+        const float2 h = hits[slot];
+        closest = h.x;
+        index = __float_as_int(h.y);
+    }
     V3 o, d, T, C;
     if (FIRST) {
         o = S.cam;
@@ -513,6 +519,15 @@ __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &p
         d = v3(r0.w, r1.x, r1.y);
         T = v3(r1.z, r1.w, r2.x);
         C = v3(r2.y, r2.z, r2.w);
+    }
+    if (INLINE) {
+        closest = 1e30f;
+        index = -1;
+        for (int i = 0; i < S.sphere_count; i++) {
+            const float4 sph = S.spheres[i];
+            float t;
+            if (ray_sphere(o, d, v3(sph.x, sph.y, sph.z), sph.w, closest, t)) { closest = t; index = i; }
+        }
     }
     V3 no = o, nd = d;
     if (index == -1) {
@@ -539,7 +554,7 @@ __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &p
 // Ray state lives in slot order (the reorder moves it), so every access here is coalesced.  A
 // ray's radiance goes to acc[ray id] (pixel-major, what accumulation reads) when it terminates
 // or after the last bounce.
-template <bool SORTED, bool COUNT, int FIRST, bool FUSED>
+template <bool SORTED, bool COUNT, int FIRST, bool FUSED, bool INLINE>
 __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
                                                        float4 *__restrict__ tc, const uint32_t *__restrict__ rid,
                                                        float4 *__restrict__ acc, uint8_t *__restrict__ bkt,
@@ -551,7 +566,7 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
     for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
         const int slot = base + threadIdx.x;
         if (slot >= L) continue;
-        const Shaded sh = shade_one<SORTED, FIRST>(S, pa, slot, geo, tc, rid, hits, seed_term);
+        const Shaded sh = shade_one<SORTED, FIRST, INLINE>(S, pa, slot, geo, tc, rid, hits, seed_term);
         const V3 no = sh.no, nd = sh.nd, T = sh.T, C = sh.C;
         miss += sh.kind == 0;
         hit += sh.kind != 0;
@@ -565,6 +580,17 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
         if (dead || last) acc[sh.ray] = tcv;
         else if (!FUSED) tc[slot] = tcv;   // FUSED: the reorder replays the shading instead
         if (!last) bkt[slot] = (uint8_t)(dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u));
+    }
+    if (INLINE) {   // no trace kernel ran: the live segments (and the root pop, the sphere tests) count here
+        Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
+        const unsigned long long nl = wave_sum(hit + miss);
+        if (lane_id() == 0 && nl) {
+            atomicAdd(&cs->live, nl);
+            if (COUNT) {
+                atomicAdd(&cs->pn, nl);
+                atomicAdd(&cs->st, nl * (unsigned long long)S.sphere_count);
+            }
+        }
     }
     if (COUNT) {
         Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
@@ -732,7 +758,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
 // terminated rays); this replays the live rays' shading from the same inputs (shade_one is
 // deterministic) and writes the new state straight to its sorted slot, saving the shade
 // kernel's 48-B state write and the plain scatter's 48-B read per live ray.
-template <bool SORTED, int FIRST>
+template <bool SORTED, int FIRST, bool INLINE>
 __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, PassArgs pa,
                                                                     const uint8_t *__restrict__ bkt_in,
                                                                     const float4 *__restrict__ geo_in,
@@ -766,7 +792,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
             const uint32_t b = valid ? bkt_in[item] : 0u;
             const bool move = valid && b != kDead;
             Shaded sh{};
-            if (move) sh = shade_one<SORTED, FIRST>(S, pa, item, geo_in, tc_in, rid_in, hits, seed_term);
+            if (move) sh = shade_one<SORTED, FIRST, INLINE>(S, pa, item, geo_in, tc_in, rid_in, hits, seed_term);
             const unsigned long long peers = match_bucket(b, valid);
             const uint32_t rank = rank_below(peers);
             if (valid && rank == 0) wcount[wave][b] = (uint32_t)__popcll(peers);
@@ -976,6 +1002,9 @@ struct rt_renderer {
     // traffic it saves (teapot 7.73 -> 7.79).  On for scenes of <= RT_FUSED_MAX_TRIS triangles;
     // RTAMD_FUSED=0/1 overrides.
     bool fused = false;
+    // No triangles (spheres.scene): no trace kernel; the sphere loop runs inside the fused
+    // shade/reorder (INLINE), saving the hit round trip and the trace launch per bounce.
+    bool inline_hits = false;
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
     DevBuf<float4> spheres, tris, mats, nodes;
@@ -1016,6 +1045,8 @@ struct rt_renderer {
         tile_rows = o->tile_rows > 0 ? o->tile_rows : 8;
         fused = sc->triangle_count <= RT_FUSED_MAX_TRIS;
         if (const char *f = std::getenv("RTAMD_FUSED")) fused = std::atoi(f) != 0;
+        inline_hits = fused && sc->triangle_count == 0;
+        if (const char *f = std::getenv("RTAMD_INLINE")) inline_hits = fused && std::atoi(f) != 0 && sc->triangle_count == 0;
         if (tile_index < 0 || tile_index >= tile_count)
             return rtamd::fail(RT_E_INVALID, "tile_index outside [0, tile_count)");
         if (tile_count > 1 && sort)
@@ -1215,15 +1246,20 @@ struct rt_renderer {
             const bool last = b + 1 == bounces;
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
-        hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,        \
-                           c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                                   \
-        if (fused)                                                                                               \
-            hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
-                               pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
+        if (!inline_hits)                                                                                        \
+            hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                               \
+        if (inline_hits)                                                                                         \
+            hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
+                               ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,  \
+                               seed_term, (int)last, ctr.p);                                                     \
+        else if (fused)                                                                                          \
+            hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, false>), dim3(sgrid), dim3(kBlock), 0, \
+                               st, ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
                                seed_term, (int)last, ctr.p);                                                     \
         else                                                                                                     \
-            hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, false>), dim3(sgrid), dim3(kBlock), 0, st, ds,\
-                               pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
+            hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, false, false>), dim3(sgrid), dim3(kBlock), 0, \
+                               st, ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
                                seed_term, (int)last, ctr.p);                                                     \
     } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
@@ -1255,16 +1291,18 @@ struct rt_renderer {
                 hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, lv, tiles,
                                    c.sort_offsets.p, c.sort_totals.p, c.live.p + b + 1);
                 if (fused) {
-#define RT_FSC(SO, FI)                                                                                           \
-    hipLaunchKernelGGL((sort_scatter_shade_kernel<SO, FI>), dim3(sort_grid), dim3(kBlock), 0, st, ds, pa, c.bkt.p, \
-                       c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.hits.p, seed_term, lv, tiles, c.sort_offsets.p,  \
-                       c.sort_totals.p, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p)
+#define RT_FSC2(SO, FI, IN)                                                                                      \
+    hipLaunchKernelGGL((sort_scatter_shade_kernel<SO, FI, IN>), dim3(sort_grid), dim3(kBlock), 0, st, ds, pa,     \
+                       c.bkt.p, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.hits.p, seed_term, lv, tiles,          \
+                       c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p)
+#define RT_FSC(SO, FI) do { if (inline_hits) RT_FSC2(SO, FI, true); else RT_FSC2(SO, FI, false); } while (0)
                     if (sort) {
                         if (b == 0) RT_FSC(true, 1); else RT_FSC(true, 0);
                     } else {
                         if (b == 0 && tiled()) RT_FSC(false, 2); else if (b == 0) RT_FSC(false, 1); else RT_FSC(false, 0);
                     }
 #undef RT_FSC
+#undef RT_FSC2
                 } else if (b == 0 && tiled())
                     hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
                                        c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
