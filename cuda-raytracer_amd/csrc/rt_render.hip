@@ -997,14 +997,17 @@ struct rt_renderer {
     // marker packets per bounce in every pass's stream; off, a frame runs ~2 % faster
     bool pass_events = true;
     // Fused reorder: shade writes only buckets and the scatter replays the shading (no 48-B state
-    // round trip per live ray).  It pays where traversal is cheap and the bounce is HBM-streaming
-    // bound (spheres: 3.82 -> 3.52 ms/pass); with a big BVH the replay costs more than the
-    // traffic it saves (teapot 7.73 -> 7.79).  On for scenes of <= RT_FUSED_MAX_TRIS triangles;
-    // RTAMD_FUSED=0/1 overrides.
+    // round trip per live ray).  It pays where the bounce is HBM-streaming bound: every bounce of
+    // a scene with cheap traversal (spheres: 3.82 -> 3.52 ms/pass), and bounce 0 of a big one
+    // (all rays live, primary rays cheap to replay: teapot 7.68 -> 7.49, lamp 15.33 -> 15.10);
+    // at later bounces of a big BVH the replay costs more than the traffic it saves (teapot,
+    // every bounce: 7.79 vs 7.73; bounces 0-1: 7.71 vs 7.61 for bounce 0 alone).  RTAMD_FUSED:
+    // 0 never, 1 every bounce, k >= 2 bounces <= k - 2.
     bool fused = false;
     // No triangles (spheres.scene): no trace kernel; the sphere loop runs inside the fused
     // shade/reorder (INLINE), saving the hit round trip and the trace launch per bounce.
     bool inline_hits = false;
+    int fused_upto = -1;              // fused reorder at bounces <= this (when not `fused`)
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
     DevBuf<float4> spheres, tris, mats, nodes;
@@ -1044,7 +1047,12 @@ struct rt_renderer {
         tile_index = o->tile_index;
         tile_rows = o->tile_rows > 0 ? o->tile_rows : 8;
         fused = sc->triangle_count <= RT_FUSED_MAX_TRIS;
-        if (const char *f = std::getenv("RTAMD_FUSED")) fused = std::atoi(f) != 0;
+        fused_upto = fused ? -1 : 0;
+        if (const char *f = std::getenv("RTAMD_FUSED")) {
+            const int v = std::atoi(f);
+            fused = v == 1;
+            fused_upto = v >= 2 ? v - 2 : -1;
+        }
         inline_hits = fused && sc->triangle_count == 0;
         if (const char *f = std::getenv("RTAMD_INLINE")) inline_hits = fused && std::atoi(f) != 0 && sc->triangle_count == 0;
         if (tile_index < 0 || tile_index >= tile_count)
@@ -1253,7 +1261,7 @@ struct rt_renderer {
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
                                ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,  \
                                seed_term, (int)last, ctr.p);                                                     \
-        else if (fused)                                                                                          \
+        else if (fused || b <= fused_upto)                                                                       \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, false>), dim3(sgrid), dim3(kBlock), 0, \
                                st, ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
                                seed_term, (int)last, ctr.p);                                                     \
@@ -1290,7 +1298,7 @@ struct rt_renderer {
                                    c.sort_counts.p);
                 hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, lv, tiles,
                                    c.sort_offsets.p, c.sort_totals.p, c.live.p + b + 1);
-                if (fused) {
+                if (fused || b <= fused_upto) {
 #define RT_FSC2(SO, FI, IN)                                                                                      \
     hipLaunchKernelGGL((sort_scatter_shade_kernel<SO, FI, IN>), dim3(sort_grid), dim3(kBlock), 0, st, ds, pa,     \
                        c.bkt.p, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.hits.p, seed_term, lv, tiles,          \

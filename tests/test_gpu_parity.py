@@ -149,7 +149,7 @@ def test_run_host_pass_sums(gpu):
     r.close()
 
 
-@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("fused", ["0", "1", "2", "3"])   # never, every bounce, bounce 0, bounces 0-1
 @pytest.mark.parametrize("scene,image,sort", [("teapot", (96, 54, 20, 16), True), ("cornell_plus", (48, 48, 20, 8), False),
                                               ("spheres", (64, 48, 20, 8), True)])
 def test_fused_and_plain_reorder_bitexact(gpu, monkeypatch, scene, image, sort, fused):

@@ -1,6 +1,6 @@
 """Interleaved A/B of librtamd.so variants (run on the GPU box after tools/variants.sh here).
 
-    python tools/ab.py ROUNDS name1 name2 ... [-- extra bench args]
+    python tools/ab.py ROUNDS name1 name2 ... [-- extra bench args]      (name: variant[@VAR=v,...])
 Each round runs bench.py once per variant (RTAMD_LIB points at build_var/<name>), in order, so
 device/clock drift hits every variant alike; prints median/min ms_per_step and process ms."""
 import json
@@ -22,10 +22,15 @@ def main():
     res = {n: [] for n in names}
     for r in range(rounds):
         for n in names:
-            lib = os.path.join(REPO, "cuda-raytracer_amd", "build_var", n, "librtamd.so")
-            if n == "default":
+            # "name@VAR=v,VAR2=w": library variant `name` (or "default") with extra environment
+            base, _, extra_env = n.partition("@")
+            lib = os.path.join(REPO, "cuda-raytracer_amd", "build_var", base, "librtamd.so")
+            if base == "default":
                 lib = os.path.join(REPO, "cuda-raytracer_amd", "build", "librtamd.so")
             env = dict(os.environ, RTAMD_LIB=lib)
+            for kv in filter(None, extra_env.split(",")):
+                k, _, v = kv.partition("=")
+                env[k] = v
             out = subprocess.run([sys.executable, "bench.py", "--no-cpu-baseline", "--no-counters"] + extra,
                                  cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
