@@ -26,14 +26,18 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-# The renderer keeps up to 16 passes in flight on their own streams; HIP's default of 4 hardware
-# queues would make them share queues.  With torch.distributed (RCCL) in the process its streams
-# need queues too: 16 queues cost the 1-GPU --dist run 11 % (8.61 vs 7.83 ms/pass), 24 nothing.
-# Set before HIP initialises.
+# The renderer keeps up to 20 passes in flight on their own streams; HIP's default of 4 hardware
+# queues would make them share queues (20 in flight: 24 queues beat 16 by 1.5 % on teapot, 3.4 %
+# on lamp).  With torch.distributed (RCCL) in the process its streams need queues too (16 passes
+# and 16 queues cost the 1-GPU --dist run 11 %).  Set before HIP initialises.
 _DIST = int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dist" in sys.argv
-_QUEUES = 24 if _DIST else 16
+_QUEUES = 28 if _DIST else 24
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _QUEUES:
     os.environ["GPU_MAX_HW_QUEUES"] = str(_QUEUES)
+# Next to RCCL, 16 passes in flight beat 20 (1-GPU --dist: 7.63 vs 7.76 ms/pass for a frame, 8.10
+# vs 9.0-12.7 for a 13-pass share); alone, 20 are faster.
+if _DIST:
+    os.environ.setdefault("RTAMD_INFLIGHT", "16")
 sys.path.insert(0, os.path.join(REPO, "cuda-raytracer_amd"))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 
@@ -272,7 +276,7 @@ def main():
         roof = None
         if counted:
             bytes_launch = bytes_total / launches
-            # Up to 16 passes are in flight, so process launches of different passes overlap and a
+            # Up to 20 passes are in flight, so process launches of different passes overlap and a
             # launch's own duration overstates its share of the GPU: `achieved` is the process
             # kernels' algorithmic bytes over the wall time of the timed steps (conservative: the
             # wall also covers reorder/accumulate); the per-launch figure is reported too.

@@ -80,9 +80,9 @@ int render_multi(const rt_scene *s, int sort, int ndev, std::vector<float> &fb, 
 }  // namespace
 
 int main(int argc, char **argv) {
-    // Up to 16 passes in flight per device on their own streams: give HIP enough hardware queues
+    // Up to 20 passes in flight per device on their own streams: give HIP enough hardware queues
     // (read when HIP initialises).
-    if (const char *q = std::getenv("GPU_MAX_HW_QUEUES"); !q || std::atoi(q) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+    if (const char *q = std::getenv("GPU_MAX_HW_QUEUES"); !q || std::atoi(q) < 24) setenv("GPU_MAX_HW_QUEUES", "24", 1);
     if (argc < 2) {
         std::printf("Usage: %s <scene>\n", argv[0]);
         return 1;

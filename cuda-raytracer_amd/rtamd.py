@@ -13,10 +13,10 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 BUILD_DIR = os.path.join(PKG_DIR, "build")
-# Up to 16 passes in flight on their own streams: ask HIP for enough hardware queues (effective
+# Up to 20 passes in flight on their own streams: ask HIP for enough hardware queues (effective
 # only if HIP has not initialised in this process yet).
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(BUILD_DIR, "librtamd.so")  # env: A/B builds only
 CLI_PATH = os.path.join(BUILD_DIR, "raytracing")
 HEADER = os.path.join(REPO, "include", "rt_abi.h")

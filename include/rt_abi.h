@@ -144,7 +144,7 @@ int rt_device_warmup(int32_t device);
 int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stats *stats);
 
 /* Persistent renderer: scene resident in HBM, ray buffers sized for 20 rays/pixel per pass,
- * up to 16 passes in flight on separate streams (each with its own buffer set) so one pass's
+ * up to 20 passes in flight on separate streams (each with its own buffer set) so one pass's
  * latency-bound last bounces overlap another's throughput-bound first bounces.  The framebuffer
  * adds stay in pass order.  Used by rt_render, the benchmark and the multi-GPU drivers. */
 typedef struct rt_renderer rt_renderer;
