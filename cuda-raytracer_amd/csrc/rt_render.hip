@@ -52,7 +52,10 @@ namespace {
 #define RT_INFLIGHT 20                // with 24 HW queues: +1.5 % teapot, +3.4 % lamp over 16 (24 in flight: worse)
 #endif
 #ifndef RT_TRACE_OCC
-#define RT_TRACE_OCC 40
+#define RT_TRACE_OCC 0                // fixed % of the resident trace workgroups (0: adaptive, below)
+#endif
+#ifndef RT_TRACE_OCC_MIN
+#define RT_TRACE_OCC_MIN 15
 #endif
 #ifndef RT_QUEUES
 #define RT_QUEUES 8
@@ -79,7 +82,11 @@ constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are i
 constexpr int kRefillFirst = RT_REFILL_FIRST;   // same at bounce 0: a whole wave of consecutive primary rays
                                                 // (~3 pixels) starts together and stays in lockstep
 constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffer set each)
-constexpr int kTraceOccPct = RT_TRACE_OCC; // % of the resident trace workgroups the persistent grid uses
+// Persistent trace grid as a % of the resident trace workgroups: the passes in flight share the
+// chip, so each pass's trace takes 200 % / (passes in flight), at least RT_TRACE_OCC_MIN and at most
+// 100 % (20 in flight: 15 %; A/B at 20 in flight: 40 % 7.51, 30 % 7.41, 20 % 7.37, 15 % 7.33,
+// 10 % 7.35 ms/pass; lamp and the 13-pass share also best at 15 %).
+constexpr int kTraceOccPct = RT_TRACE_OCC;
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
 constexpr int kQueueStride = 64;     // words between shards (256 B: one shard per cache line)
 constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFFFFF)
@@ -1016,7 +1023,8 @@ struct rt_renderer {
     DevBuf<float> env, fb;
     DevBuf<Counters> ctr;
     PassCtx ctx[kInflight];
-    int trace_blocks = 0;             // persistent trace_kernel grid
+    int trace_blocks = 0;             // persistent trace_kernel grid of the current run
+    int trace_blocks_max = 0;         // all resident trace workgroups (the overflow stacks are sized for it)
     int nctx = 1;                     // pass contexts allocated (passes in flight)
     int cus = 0;
     hipEvent_t t_begin = nullptr, t_end = nullptr;
@@ -1148,12 +1156,13 @@ struct rt_renderer {
         tm.mark("scene upload");
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<true, false, false>, kBlock, 0));
         tm.mark("occupancy query");
-        trace_blocks = std::max(1, cus * std::max(1, per_cu) * kTraceOccPct / 100);
+        trace_blocks_max = std::max(1, cus * std::max(1, per_cu));
+        trace_blocks = trace_blocks_max;
         const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
         // than half of the free device memory holds (1080p: ~2.9 GB per context).
         const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8) +
-                                 (size_t)trace_blocks * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
+                                 (size_t)trace_blocks_max * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
         size_t mem_free = 0, mem_total = 0;
         HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
         // RTAMD_INFLIGHT caps the passes in flight below kInflight (bench.py: 16 next to RCCL, where
@@ -1179,7 +1188,7 @@ struct rt_renderer {
             if ((rc = c.live.alloc((size_t)bounces + 1))) return rc;
             if ((rc = c.queue.alloc((size_t)(bounces + 1) * kQueues * kQueueStride))) return rc;
             if ((rc = c.hits.alloc((size_t)max_rays))) return rc;
-            if ((rc = c.overflow.alloc((size_t)trace_blocks * kBlock * 2 * (kStackMax - kStackLds)))) return rc;
+            if ((rc = c.overflow.alloc((size_t)trace_blocks_max * kBlock * 2 * (kStackMax - kStackLds)))) return rc;
             if ((rc = c.psum.alloc((size_t)pixels * 3))) return rc;
         }
         tm.mark("pass contexts");
@@ -1414,6 +1423,12 @@ struct rt_renderer {
         if (pass_begin < 0 || (count > 0 && pass_begin + (int64_t)(count - 1) * stride >= P))
             return rtamd::fail(RT_E_INVALID, "pass range outside the render");
         const int inflight = std::min(nctx, std::max(1, P));
+        {   // the trace grid of this run, for the passes it actually keeps in flight
+            const int concurrent = std::max(1, std::min(inflight, count));
+            const int pct = kTraceOccPct > 0 ? kTraceOccPct
+                                             : std::min(100, std::max(RT_TRACE_OCC_MIN, 200 / concurrent));
+            trace_blocks = std::max(1, trace_blocks_max * pct / 100);
+        }
         hipStream_t s0 = stream();
         HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, s0));
         HIPCHK(hipEventRecord(t_begin, s0));
