@@ -14,9 +14,13 @@ full frame (strong scaling); `--steps K` times K passes per GPU (weak scaling).
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line.  `value` = live ray segments (process_ray calls on live slots)
-per second over all GPUs, inputs resident in HBM.  `roofline` prices the dominant kernel
-(process_kernel) with SURVEY.md §8(d)'s logical byte model; `cpu_baseline` times the
-oracle's restatement of the reference `cpu` path on a bounded sample on the host cores.
+per second over all GPUs, inputs resident in HBM.  `render_wall_ms` = one full frame (the
+metric's second column); `bit_exact_vs_oracle` = this run's pass-0 framebuffer hashed against
+the oracle's (tests/golden/bench_pass0.json).  `roofline` prices the dominant kernel
+(trace_kernel) per launch: algorithmic HBM bytes and the measured PMC traffic against HBM,
+SURVEY.md §8(d)'s logical cache-inclusive bytes against the L2; `cpu_baseline` times the
+oracle's restatement of the reference `cpu` path on the host cores (§8(d): first pass +
+remainder pass, extrapolated).
 """
 import argparse
 import json
@@ -57,53 +61,99 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 TILE_ROWS = 8          # pixel-tile stripe height (--shard tiles; SURVEY §8e: interleaved 8-row stripes)
 
 
-def segment_bytes(st, spheres):
-    """SURVEY.md §8(d) logical bytes of the process kernel, summed over the counted launches."""
-    live = st["live_segments"]
-    hits, hs = st["hits"], st["hits_sphere"]
-    b = live * (8 + 48 + 48 + 4 + 16 * spheres)
-    b += 32 * st["nodes_popped"] + 64 * st["internal_visits"] + 48 * st["triangle_tests"]
-    b += hits * (2 + 48) + (hits - hs) * 48 + hs * 16 + st["misses"] * 12
-    # §8(d) also charges 8 B per terminated slot; this kernel never touches those slots when the
-    # reorder is on (it walks only the live prefix), and reads a 1-B bucket per slot when off.
-    b += st.get("dead_slot_bytes", 0)
-    return b
+L2_PEAK_GBS = 34500.0  # MI355X aggregate L2 (8 XCDs x 4 MiB), MI355X_MICROARCH.md §L2: ~34.5 TB/s
+
+
+def logical_trace_bytes(st, spheres):
+    """SURVEY.md §8(d)'s logical (cache-inclusive) bytes of the traversal part of process_ray over
+    the counted launches: per live segment the ray (24 B) and S spheres, 32 B per node pop, 64 B
+    per internal visit (two child nodes), 48 B per triangle test, 8 B hit written."""
+    return (st["live_segments"] * (24 + 16 * spheres + 8) + 32 * st["nodes_popped"] +
+            64 * st["internal_visits"] + 48 * st["triangle_tests"])
+
+
+def compulsory_trace_bytes(st, scene_bytes, launches):
+    """Algorithmic HBM bytes of the trace launches: what a launch cannot avoid moving from or to
+    HBM.  Each live segment's ray (o, d: 24 B) is read once, except at bounce 0 where the primary
+    ray is computed in place (every generated ray is live there); its hit {t, index} (8 B) is
+    written once; the scene's node and triangle arrays (reference layouts, 32 B / 48 B / 16 B per
+    sphere) are read once per launch."""
+    live, gen = st["live_segments"], st["generated_rays"]
+    return 24 * (live - gen) + 8 * live + launches * scene_bytes
 
 
 def load_pmc(workload):
-    """HBM traffic per process_kernel launch from the committed rocprofv3 PMC summary."""
-    path = os.path.join(REPO, "profiles", "pmc_process_kernel.json")
+    """Measured HBM-side traffic for this workload from the committed rocprofv3 PMC summary
+    (tools/pmc.sh + tools/pmc_summary.py, one profiled pass)."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("workload") != workload:
+    d = d.get(workload)
+    if d:
+        d["file"] = "profiles/pmc_traffic.json"
+    return d
+
+
+def load_golden(scene, sort):
+    path = os.path.join(REPO, "tests", "golden", "bench_pass0.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("%s sort=%s" % (scene, "on" if sort else "off"))
+    except (OSError, ValueError):
         return None
-    return d.get("hbm_bytes_per_launch")
+
+
+def run_cpu(exe, cfg, spp, pass_limit, threads):
+    scene, w, h, _, bounces = cfg[:5]
+    cmd = [exe, os.path.join(rtamd.ASSETS, scene), rtamd.ASSETS, str(w), str(h), str(spp), str(bounces),
+           str(pass_limit), str(threads)]
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, env=env).stdout
+    return json.loads(out.strip().splitlines()[-1])
 
 
 def cpu_baseline(cfg, args):
-    """Times the oracle's restatement of cpu_raytrace (raytracing.cu:122-163) on a bounded
-    sample of the same scene: full resolution, `--cpu-spp` rays/pixel, same bounces."""
+    """Times the oracle's restatement of cpu_raytrace (raytracing.cu:122-163, OpenMP
+    schedule(dynamic, 1000) at :136,144, bounce-invariant seed :148; built with the reference's
+    -O3 -ffast-math -fopenmp) as SURVEY.md §8(d) specifies: configs of up to 4 passes in full,
+    larger ones as the first full 20-spp pass plus the remainder pass, extrapolated linearly to
+    the frame (passes cost the same: the remainder pass is the only short one)."""
     exe = os.path.join(REPO, "oracle", "build", "cpu_baseline")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    scene, w, h, _, bounces = cfg[:5]
-    cmd = [exe, os.path.join(rtamd.ASSETS, scene), rtamd.ASSETS, str(w), str(h), str(args.cpu_spp),
-           str(bounces), "1", str(threads)]
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-    out = subprocess.run(cmd, check=True, capture_output=True, text=True, env=env).stdout
-    rec = json.loads(out.strip().splitlines()[-1])
+    nproc = os.cpu_count() or 1
+    # the GPU pool sets OMP_NUM_THREADS to the box's CPU share for one GPU (16); elsewhere: nproc
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = args.cpu_threads or env_threads or nproc
+    scene, w, h, spp, bounces = cfg[:5]
+    P = -(-spp // 20)
+    if P <= 4:
+        rec = run_cpu(exe, cfg, spp, -1, threads)
+        secs, live = rec["seconds"], rec["live_segments"]
+        sample = "%s %dx%d %d spp %d bounces, the whole frame (%d passes): %.2f s" % (scene, w, h, spp, bounces, P, secs)
+    else:
+        first = run_cpu(exe, cfg, spp, 1, threads)                  # pass 0: 20 spp
+        rem = spp - 20 * (P - 1)
+        last = run_cpu(exe, cfg, rem, 1, threads)                   # the remainder pass (remaining = 0)
+        secs = first["seconds"] * (P - 1) + last["seconds"]
+        live = first["live_segments"] * (P - 1) + last["live_segments"]
+        sample = ("%s %dx%d %d bounces: first full 20-spp pass %.2f s + remainder %d-spp pass %.2f s, timed; "
+                  "frame of %d passes extrapolated linearly: %.1f s" % (scene, w, h, bounces, first["seconds"], rem,
+                                                                      last["seconds"], P, secs))
     return {
-        "value": round(rec["live_segments"] / rec["seconds"] / 1e6, 3),
+        "value": round(live / secs / 1e6, 3),
         "unit": "Mrays/s",
-        "cores": rec["threads"],
+        "cores": threads,
         "kind": "port",
-        "sample": "%s %dx%d, %d spp (one pass), %d bounces: %d live segments in %.2f s "
-                  "(oracle cpu_raytrace restatement, -O3 -ffast-math -fopenmp)" % (
-                      scene, w, h, args.cpu_spp, bounces, rec["live_segments"], rec["seconds"]),
+        "sample": sample + " (oracle cpu_raytrace restatement, -O3 -ffast-math -fopenmp, %d OpenMP threads)" % threads,
+        "frame_s": round(secs, 3),
+        "extrapolated": P > 4,
+        "host_nproc": nproc,
+        "threads_from": "--cpu-threads" if args.cpu_threads else ("OMP_NUM_THREADS (the pool's CPU share per GPU)"
+                                                                  if env_threads else "nproc"),
     }
 
 
@@ -115,9 +165,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--scene", default="teapot", choices=sorted(CONFIGS))
     ap.add_argument("--no-sort", action="store_true")
-    ap.add_argument("--cpu-spp", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-counters", action="store_true", help="skip the byte-model counting rerun")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="only the warmup and timed steps (profiling: --steps 1 --warmup 0 renders exactly one pass)")
     ap.add_argument("--dist", action="store_true", help="use the torch.distributed path even at N=1")
     ap.add_argument("--shard", choices=("passes", "tiles"), default="passes",
                     help="multi-GPU decomposition: whole passes per GPU (exact in both sort modes) or "
@@ -125,6 +177,8 @@ def main():
     ap.add_argument("--tile-share", type=int, default=0, metavar="N",
                     help="1-GPU probe of --shard tiles: render only rank 0's stripes of an N-GPU split")
     args = ap.parse_args()
+    if args.no_extras:
+        args.no_counters = args.no_cpu_baseline = True
     # The JSON line is the only thing on stdout: native libraries (RCCL prints a version banner)
     # write to stdout too, so fd 1 is pointed at stderr and the line goes to a saved copy of it.
     json_out = os.fdopen(os.dup(1), "w")
@@ -226,8 +280,16 @@ def main():
             stats[key] = stats.get(key, 0) + v
         return mine
 
-    # No per-bounce HIP events in the timed steps (four marker packets per bounce in every pass's
-    # stream cost ~2 %); the kernel-time split comes from an untimed re-run below.
+    def reduce(vals, op="sum"):
+        """Sum (or max) of per-rank floats over the ranks (every rank calls it)."""
+        if not use_dist:
+            return list(vals)
+        t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        return [float(x) for x in t.tolist()]
+
+    # No per-bounce HIP events in the timed steps (five marker packets per bounce in every pass's
+    # stream cost ~2 %); the per-launch kernel times come from an untimed re-run below.
     ren.set_event_timing(False)
     warm = {}
     run_steps(args.warmup, warm)
@@ -238,75 +300,87 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
 
-    live = timed.get("live_segments", 0)
-    # Kernel-time split (process / reorder launches, HIP events on each pass's stream): the same
-    # steps again, untimed, with events on.
-    ren.set_event_timing(True)
-    evrun = {}
-    run_steps(steps, evrun)
-    ren.set_event_timing(False)
-    proc_ms = evrun.get("process_ms", 0.0)
-    if use_dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        t = torch.tensor([live], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t)
-        live = int(t.item())
-
-    # Byte model: recount the timed passes with the counting kernel variant (untimed).
-    counted = None
-    if not args.no_counters and steps > 0:
-        ren.set_counters(True)
-        counted = {}
-        run_steps(steps, counted)
-        counted = {k: int(v) for k, v in counted.items() if isinstance(v, int)}
-        counted["dead_slot_bytes"] = 0   # terminated slots are never visited (reorder or live list)
-        ren.set_counters(False)
-    bytes_total = segment_bytes(counted, scene.view.sphere_count) if counted else 0.0
-    launches = my_passes * bounces
-    if use_dist:
-        t = torch.tensor([bytes_total, launches], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t)
-        bytes_total, launches = float(t[0].item()), int(t[1].item())
+    # ---- untimed legs (every rank takes part: they contain collectives)
+    evrun, counted, frame_s, parity = {}, None, None, None
+    if not args.no_extras:
+        # per-launch kernel times: the same steps again with per-bounce HIP events on each pass's stream
+        ren.set_event_timing(True)
+        run_steps(steps, evrun)
+        ren.set_event_timing(False)
+        if not args.no_counters and steps > 0:
+            # byte model: the same steps with the counting kernel variant
+            ren.set_counters(True)
+            counted = {}
+            run_steps(steps, counted)
+            counted = {k: int(v) for k, v in counted.items() if isinstance(v, int)}
+            ren.set_counters(False)
+        if full_frame:
+            frame_s = elapsed
+        else:
+            # the metric's render-wall column is a full frame: time one (untimed for `value`)
+            barrier_sync()
+            f0 = time.perf_counter()
+            run_steps(R, {})
+            barrier_sync()
+            frame_s = time.perf_counter() - f0
+        if not tiles and rank == 0:
+            # parity: pass 0 of this workload, hashed against the oracle's (tests/golden/bench_pass0.json)
+            import hashlib
+            ren.clear()
+            ren.run(pass_begin=0, count=1, stride=1)
+            digest = hashlib.sha256(ren.framebuffer().astype("<f4").tobytes()).hexdigest()
+            gold = load_golden(args.scene, sort)
+            parity = {"bit_exact_vs_oracle": (digest == gold["sha256"]) if gold else None,
+                      "sha256_pass0": digest,
+                      "oracle": "tests/golden/bench_pass0.json (CPU oracle, tests/golden/make_bench_hashes.py)"
+                      if gold else "no golden hash for this workload",
+                      "reference_rms": "parity unpinned: the reference's GPU path cannot run here (SURVEY.md §8c), "
+                                       "the oracle is a cited restatement; image error vs the reference is not measured"}
+    elapsed, frame_s_max = reduce([elapsed, frame_s or 0.0], "max")
+    live, gen = reduce([timed.get("live_segments", 0), timed.get("generated_rays", 0)])
 
     if rank == 0:
         workload = "%s %dx%d %dspp %d bounces sort=%s" % (scene_file, W, H, spp, bounces, "on" if sort else "off")
-        ms_launch = proc_ms / (my_passes * bounces) if my_passes else 0.0
+        v = scene.view
+        scene_bytes = 32 * v.bvh_node_count + 48 * v.triangle_count + 16 * v.sphere_count
+        launches = int(evrun.get("trace_launches", 0))
+        trace_ms = evrun.get("trace_ms", 0.0) / launches if launches else 0.0
         roof = None
-        if counted:
-            bytes_launch = bytes_total / launches
-            # Up to 20 passes are in flight, so process launches of different passes overlap and a
-            # launch's own duration overstates its share of the GPU: `achieved` is the process
-            # kernels' algorithmic bytes over the wall time of the timed steps (conservative: the
-            # wall also covers reorder/accumulate); the per-launch figure is reported too.
-            achieved = bytes_total / elapsed / 1e9 if elapsed > 0 else 0.0
-            per_launch = bytes_launch / (ms_launch / 1e3) / 1e9 if ms_launch > 0 else 0.0
-            traffic = load_pmc(workload)
-            # measured HBM-side bytes (rocprofv3 PMC, per trace+shade launch) over the same launches
-            hbm_gbs = traffic * launches / elapsed / 1e9 if traffic and elapsed > 0 else None
+        if counted and launches and trace_ms > 0:
+            # this rank's counted launches (the same steps as the event re-run)
+            comp = compulsory_trace_bytes(counted, scene_bytes, launches) / launches
+            logical = logical_trace_bytes(counted, v.sphere_count) / launches
+            achieved = comp / (trace_ms / 1e3) / 1e9
+            pmc = load_pmc(workload)
+            traffic = pmc["trace_bytes_per_launch"] if pmc else None
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "hbm_measured_gbs": round(hbm_gbs, 1) if hbm_gbs else None,
-                    "hbm_measured_frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
-                    "note": "achieved/frac: SURVEY.md 8(d) logical bytes (every BVH node and triangle fetch counted, "
-                            "cache-inclusive) over the render wall; frac > 1 means the traversal working set is "
-                            "served by L2/Infinity Cache. traffic: measured L2->fabric bytes per trace+shade launch "
-                            "(profiles/pmc_process_kernel.json); hbm_measured_*: that traffic over the same wall",
-                    "kernel": "process (trace_kernel + shade_kernel per bounce)",
-                    "bytes_per_launch": int(bytes_launch), "ms_per_launch": round(ms_launch, 4),
-                    "achieved_per_launch_events": round(per_launch, 1),
-                    "per_launch_events_from": "untimed re-run of the timed steps with per-bounce HIP events "
-                                              "(the timed steps record none)",
-                    "model": "SURVEY.md 8(d): per live segment 108+16S + 32*Pn + 64*Iv + 48*Tt + hit(98|66)/miss(12); "
-                             "dead slots: 0 B with sort (never visited), 1 B without; counts from the device "
-                             "counters of the same passes; achieved = bytes of all process launches / timed wall"}
+                    "kernel": "trace_kernel (BVH traversal + Moller-Trumbore + slab + sphere loop), per launch",
+                    "bytes_per_launch": int(comp), "ms_per_launch": round(trace_ms, 4), "launches": launches,
+                    "achieved_def": "algorithmic HBM bytes per trace launch (24 B ray read per live segment past "
+                                    "bounce 0 + 8 B hit write per live segment + the scene's node/triangle arrays "
+                                    "once, reference layouts) / average trace launch duration (HIP events on the "
+                                    "pass's stream, untimed re-run of the timed steps; up to 20 passes share the chip, "
+                                    "so a launch's duration includes time it shared)",
+                    "traffic_def": None if not pmc else
+                    "measured HBM-side bytes per trace launch, rocprofv3 --pmc, one profiled pass "
+                    "(%s; reads priced by request size TCC_EA0_RDREQ_{128B,64B,32B}, = 2 x FETCH_SIZE for 128-B "
+                    "requests per MI355X_MICROARCH.md §HBM; writes TCC_EA0_WRREQ{,_64B}); %s" % (pmc["file"], pmc.get("run", "")),
+                    "traffic_frac": round(traffic / (trace_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                    "l2": {"achieved": round(logical / (trace_ms / 1e3) / 1e9, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(logical / (trace_ms / 1e3) / 1e9 / L2_PEAK_GBS, 4),
+                           "bytes_per_launch": int(logical),
+                           "def": "SURVEY.md 8(d) logical cache-inclusive bytes of the traversal (24 B ray + 16 B x S "
+                                  "+ 32 B x node pops + 64 B x internal visits + 48 B x triangle tests + 8 B hit) per "
+                                  "launch / launch duration, against the aggregate L2 rate (MI355X_MICROARCH.md §L2)"}}
+            if pmc and pmc.get("pass_bytes"):
+                ms_pass = elapsed / max(steps, 1) * 1e3
+                roof["frame"] = {"hbm_bytes_per_pass": pmc["pass_bytes"], "ms_per_pass": round(ms_pass, 3),
+                                 "achieved": round(pmc["pass_bytes"] / (ms_pass / 1e3) / 1e9, 1),
+                                 "frac": round(pmc["pass_bytes"] / (ms_pass / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "def": "measured HBM-side bytes of one pass (every kernel, same PMC run) / timed "
+                                        "wall per pass (one GPU's passes overlap 20 at a time)"}
         value = live / elapsed / 1e6 if elapsed > 0 else 0.0
-        gen = timed.get("generated_rays", 0)
-        if use_dist:
-            t = torch.tensor([gen], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t)
-            gen = int(t.item())
         nominal = gen * bounces / elapsed / 1e6 if elapsed > 0 else 0.0
         ms_step = elapsed / steps * 1e3 if steps else 0.0
         out = {
@@ -322,6 +396,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: reference scene + assets, procedural stand-in env map (assets missing upstream)",
+            "render_wall_ms": round(frame_s_max * 1e3, 1) if frame_s_max else None,
+            "bit_exact_vs_oracle": parity["bit_exact_vs_oracle"] if parity else None,
             "config": {
                 "workload": workload,
                 "step": ("one 20-spp pass (%d rays x %d bounces) over this GPU's %d-row pixel stripes; "
@@ -331,16 +407,19 @@ def main():
                 "parallelism": ("pixel-tile x%d (%d-row stripes) + RCCL gather" % (world, TILE_ROWS) if tiles else
                                 "pass-shard x%d + RCCL all-to-all/gather" % world) if world > 1 else "single GPU",
                 "nominal_mrays_per_s": round(nominal, 2),
-                "render_wall_ms": round(elapsed * 1e3, 1) if full_frame else None,
-                "render_wall_ms_projected": round(ms_step * R, 1),
+                "render_wall_def": "one full frame (%d passes), first pass to the accumulated framebuffer on the "
+                                   "GPU, inputs resident (%s)" % (P, "the timed region" if full_frame else
+                                                                  "an untimed full-frame leg after the timed steps"),
                 "passes_per_frame": P,
-                "process_ms_per_step": round(proc_ms / max(my_passes, 1), 3),
+                "process_ms_per_step": round(evrun.get("process_ms", 0.0) / max(my_passes, 1), 3),
+                "trace_ms_per_step": round(evrun.get("trace_ms", 0.0) / max(my_passes, 1), 3),
                 "sort_ms_per_step": round(evrun.get("sort_ms", 0.0) / max(my_passes, 1), 3),
                 "scene_load_s": round(load_s, 3),
                 "bvh_ms": round(scene.bvh_ms, 1),
                 **({"tile_share_probe": "rank 0's %d-row stripes of a %d-GPU split, on one GPU"
                     % (TILE_ROWS, args.tile_share)} if args.tile_share > 1 else {}),
             },
+            "parity": parity,
             "roofline": roof,
             "cpu_baseline": None,
         }

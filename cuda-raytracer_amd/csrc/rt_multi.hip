@@ -1,0 +1,241 @@
+// rt_multi.hip — multi-GPU rt_render in one process: pass sharding over the devices of one node,
+// framebuffer exchange over RCCL (xGMI).  SURVEY §8b (rt_opts.device_count / device_ids) and §8e
+// ("Alternative: pass sharding ... exact with sort on, zero per-bounce traffic").
+//
+// Replaces gpu_raytrace (reference raytracing.cu:170-284) when rt_opts.device_count >= 1.  The
+// reference ran one device; its pass loop (raytracing.cu:222-254) is a sequence of independent
+// 20-spp passes, each with its own generate seed, per-bounce process seeds and stable reorder,
+// so a pass renders identically on any device.
+//
+//   * Device k of N renders passes k, k+N, k+2N, ... (round-robin: passes cost the same except a
+//     shorter last one), as many in flight as its renderer keeps, into padded pass buffers.
+//   * The framebuffer is owned per pixel slice: W*H*3 floats cut into N slices of sl floats.
+//     After a chunk of rounds, one ncclAllToAll per round sends slice j of each pass buffer to
+//     device j (each xGMI link carries 1/N of the data; nothing converges on one GPU), and device
+//     j adds the slices it received in pass order, fb_j = ((0 + S_0,j) + S_1,j) + ..., exactly
+//     the per-pixel add sequence of one device: the N-device image is bit-identical to the
+//     1-device image with sort on or off.
+//   * One ncclGather of the N finished slices to device_ids[0], then one D2H copy to fb_out.
+//
+// Exchange bytes per frame: every pass buffer leaves its device except its own slice,
+// P * W*H*3*4 * (N-1)/N in all (1080p teapot, N = 8: 103 passes x 24.9 MB x 7/8 = 2.24 GB over the
+// job, ~280 MB per device, 1/7 of it per link), plus the gather's W*H*3*4 * (N-1)/N into device 0.
+// One host thread per device (RCCL's one-thread-per-device model for a single-process
+// communicator); device_count = 1 runs the same code with every exchange local.
+#include "rt_abi.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace rtamd {
+int fail(int code, const std::string &msg);
+}
+extern "C" int rtamd_renderer_run_pitched(rt_renderer *r, int pass_begin, int count, int stride,
+                                          float *d_pass_sums, size_t pitch, rt_stats *stats);   // rt_render.hip
+
+namespace {
+
+// slice[i] += recv[j][src][i] for the rounds j of the chunk and the ranks src whose pass exists,
+// in ascending pass order (pass = src + N * (k0 + j)): one lane per element, ordered adds.
+__global__ __launch_bounds__(256) void add_slices_kernel(float *__restrict__ slice, const float *__restrict__ recv,
+                                                         size_t sl, int world, int rounds, int k0, int passes) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= sl) return;
+    float acc = slice[i];
+    for (int j = 0; j < rounds; j++)
+        for (int src = 0; src < world; src++)
+            if (src + world * (k0 + j) < passes) acc = acc + recv[((size_t)j * world + src) * sl + i];
+    slice[i] = acc;
+}
+
+const char *nccl_str(ncclResult_t r) { return ncclGetErrorString(r); }
+
+struct DevState {
+    int device = 0, rank = 0;
+    int rc = 0;
+    std::string err;
+    rt_stats stats{};
+    double exchange_ms = 0;
+};
+
+int hip_err(hipError_t e, const char *what) {
+    return rtamd::fail(e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP,
+                       std::string("Error ") + what + " " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+#define MHIP(call)                                              \
+    do {                                                        \
+        const hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return hip_err(e_, #call);        \
+    } while (0)
+#define MNCCL(call)                                                                                       \
+    do {                                                                                                  \
+        const ncclResult_t r_ = (call);                                                                   \
+        if (r_ != ncclSuccess) return rtamd::fail(RT_E_HIP, std::string("Error ") + #call + " " + nccl_str(r_)); \
+    } while (0)
+
+namespace {
+
+// Device `st.rank`'s share of the frame: render, exchange, add; the root also gathers.
+int run_device(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int world, DevState &st,
+               float *fb_out) {
+    MHIP(hipSetDevice(st.device));
+    const int P = (scene->ray_count + 19) / 20;
+    const size_t px3 = (size_t)scene->width * scene->height * 3;
+    const size_t sl = (px3 + world - 1) / world;      // floats per owner slice (last one padded)
+    const size_t pitch = sl * world;                  // pass buffer rows padded to N equal slices
+    const int R = (P + world - 1) / world;            // rounds: one pass per device each
+    // rounds per exchange: all of them up to 16 (the renderer's passes in flight next to RCCL)
+    const int chunk = std::max(1, std::min(R, 16));
+    rt_opts o = *base;
+    o.device = st.device;
+    o.device_count = 0;
+    o.device_ids = nullptr;
+    o.pass_begin = 0;
+    o.pass_count = -1;
+    o.pass_stride = 1;
+    o.tile_count = 0;
+    rt_renderer *ren = nullptr;
+    int rc = rt_renderer_create(scene, &o, &ren);
+    if (rc) return rc;
+    struct Guard {
+        rt_renderer *r;
+        float *bufs[3] = {nullptr, nullptr, nullptr};
+        hipStream_t s = nullptr;
+        ~Guard() {
+            for (float *b : bufs)
+                if (b) (void)hipFree(b);
+            if (s) (void)hipStreamDestroy(s);
+            rt_renderer_destroy(r);
+        }
+    } g{ren};
+    float *&buf = g.bufs[0], *&recv = g.bufs[1], *&slice = g.bufs[2];
+    MHIP(hipMalloc(reinterpret_cast<void **>(&buf), (size_t)chunk * pitch * sizeof(float)));
+    MHIP(hipMalloc(reinterpret_cast<void **>(&recv), (size_t)chunk * pitch * sizeof(float)));
+    MHIP(hipMalloc(reinterpret_cast<void **>(&slice), (st.rank == 0 ? pitch : sl) * sizeof(float)));
+    MHIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
+    MHIP(hipMemsetAsync(buf, 0, (size_t)chunk * pitch * sizeof(float), g.s));   // padding stays 0
+    MHIP(hipMemsetAsync(slice, 0, sl * sizeof(float), g.s));
+    MHIP(hipStreamSynchronize(g.s));
+    using clk = std::chrono::high_resolution_clock;
+    for (int k0 = 0; k0 < R; k0 += chunk) {
+        const int m = std::min(chunk, R - k0);
+        // this device's passes of rounds k0 .. k0+m-1
+        const int first = st.rank + world * k0;
+        const int mine = first < P ? std::min(m, (P - 1 - first) / world + 1) : 0;
+        if (mine > 0) {
+            rt_stats s{};
+            rc = rtamd_renderer_run_pitched(ren, first, mine, world, buf, pitch, &s);
+            if (rc) return rc;
+            st.stats.live_segments += s.live_segments;
+            st.stats.generated_rays += s.generated_rays;
+            st.stats.sorted_items += s.sorted_items;
+            st.stats.nodes_popped += s.nodes_popped;
+            st.stats.internal_visits += s.internal_visits;
+            st.stats.triangle_tests += s.triangle_tests;
+            st.stats.sphere_tests += s.sphere_tests;
+            st.stats.hits += s.hits;
+            st.stats.misses += s.misses;
+            st.stats.hits_sphere += s.hits_sphere;
+            st.stats.dead_slots += s.dead_slots;
+            st.stats.passes += s.passes;
+            st.stats.kernel_ms += s.kernel_ms;
+            st.stats.process_ms += s.process_ms;
+            st.stats.sort_ms += s.sort_ms;
+            st.stats.trace_ms += s.trace_ms;
+            st.stats.trace_launches += s.trace_launches;
+        }
+        // rounds of the chunk where this device has no pass send stale rows, which the owners'
+        // adds skip (pass src + N*k does not exist)
+        const auto t0 = clk::now();
+        MNCCL(ncclGroupStart());
+        for (int j = 0; j < m; j++)
+            MNCCL(ncclAllToAll(buf + (size_t)j * pitch, recv + (size_t)j * pitch, sl, ncclFloat32, comm, g.s));
+        MNCCL(ncclGroupEnd());
+        hipLaunchKernelGGL(add_slices_kernel, dim3((unsigned)((sl + 255) / 256)), dim3(256), 0, g.s, slice, recv, sl,
+                           world, m, k0, P);
+        MHIP(hipGetLastError());
+        // the next chunk's render overwrites buf: the exchange must have read it
+        MHIP(hipStreamSynchronize(g.s));
+        st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    }
+    const auto t0 = clk::now();
+    // gather the finished slices to the root (in place: the root's own slice is block 0)
+    MNCCL(ncclGather(slice, slice, sl, ncclFloat32, 0, comm, g.s));
+    if (st.rank == 0) MHIP(hipMemcpyAsync(fb_out, slice, px3 * sizeof(float), hipMemcpyDeviceToHost, g.s));
+    MHIP(hipStreamSynchronize(g.s));
+    st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    return RT_OK;
+}
+
+}  // namespace
+
+int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stats *stats) {
+    using clk = std::chrono::high_resolution_clock;
+    const auto w0 = clk::now();
+    const int world = opts->device_count;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    std::vector<int> devs(world);
+    for (int k = 0; k < world; k++) {
+        devs[k] = opts->device_ids ? opts->device_ids[k] : k;
+        if (devs[k] < 0 || devs[k] >= ndev) return rtamd::fail(RT_E_NODEVICE, "device_ids: no such HIP device");
+        for (int j = 0; j < k; j++)
+            if (devs[j] == devs[k]) return rtamd::fail(RT_E_INVALID, "device_ids: a device is listed twice");
+    }
+    if (opts->tile_count > 1) return rtamd::fail(RT_E_INVALID, "device_count and tile_count are exclusive");
+    if (opts->pass_begin != 0 || (opts->pass_count != -1 && opts->pass_count != (scene->ray_count + 19) / 20) ||
+        opts->pass_stride > 1)
+        return rtamd::fail(RT_E_INVALID, "multi-device rt_render renders the whole frame (pass_begin 0, all passes)");
+    std::vector<ncclComm_t> comms(world);
+    MNCCL(ncclCommInitAll(comms.data(), world, devs.data()));
+    std::vector<DevState> st(world);
+    std::vector<std::thread> th;
+    for (int k = 0; k < world; k++) {
+        st[k].device = devs[k];
+        st[k].rank = k;
+        th.emplace_back([&, k]() {
+            st[k].rc = run_device(scene, opts, comms[k], world, st[k], fb_out);
+            if (st[k].rc) st[k].err = rt_last_error();
+        });
+    }
+    for (auto &t : th) t.join();
+    for (auto c : comms) (void)ncclCommDestroy(c);
+    for (auto &s : st)
+        if (s.rc) return rtamd::fail(s.rc, s.err);
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        for (auto &s : st) {
+            const rt_stats &x = s.stats;
+            stats->generated_rays += x.generated_rays;
+            stats->live_segments += x.live_segments;
+            stats->sorted_items += x.sorted_items;
+            stats->nodes_popped += x.nodes_popped;
+            stats->internal_visits += x.internal_visits;
+            stats->triangle_tests += x.triangle_tests;
+            stats->sphere_tests += x.sphere_tests;
+            stats->hits += x.hits;
+            stats->misses += x.misses;
+            stats->hits_sphere += x.hits_sphere;
+            stats->dead_slots += x.dead_slots;
+            stats->passes += x.passes;
+            stats->process_ms += x.process_ms;
+            stats->sort_ms += x.sort_ms;
+            stats->trace_ms += x.trace_ms;
+            stats->trace_launches += x.trace_launches;
+            stats->kernel_ms = std::max(stats->kernel_ms, x.kernel_ms);
+            stats->exchange_ms = std::max(stats->exchange_ms, s.exchange_ms);
+        }
+        stats->render_ms = std::chrono::duration<double, std::milli>(clk::now() - w0).count();
+    }
+    return RT_OK;
+}

@@ -30,6 +30,7 @@
 namespace rtamd {
 int fail(int code, const std::string &msg);
 }
+int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stats *stats);   // rt_multi.hip
 
 using namespace rtd;
 
@@ -1094,12 +1095,19 @@ struct rt_renderer {
         if (nn > 0 && !is_leaf(sc->bvh[0])) {
             rec[0] = 0;
             nrec = 2;                   // record 1: padding, the root has no sibling
-            std::vector<int> todo{0};
+            // (node, depth of that internal node): a visit of an internal node at depth k can leave
+            // k + 1 entries on the traversal stack, which holds kStackMax (the reference's
+            // MAX_BVH_DEPTH 30 gives at most 30, scene.cu:10); a deeper caller-supplied BVH would
+            // run past the per-lane overflow stack, so it is refused here
+            std::vector<std::pair<int, int>> todo{{0, 0}};
             int visited = 0;
             while (!todo.empty()) {
-                const int i = todo.back();
+                const int i = todo.back().first, depth = todo.back().second;
                 todo.pop_back();
                 if (++visited > nn) return rtamd::fail(RT_E_INVALID, "BVH is not a tree");
+                if (depth + 1 > kStackMax)
+                    return rtamd::fail(RT_E_INVALID, "BVH deeper than the traversal stack (" + std::to_string(kStackMax) +
+                                                     " internal levels)");
                 const rt_bvh_node &nd = sc->bvh[i];
                 if (nd.child1 < 0 || nd.child2 >= nn || nd.child1 >= nn || nd.child2 < 0)
                     return rtamd::fail(RT_E_INVALID, "BVH child index out of range");
@@ -1107,8 +1115,8 @@ struct rt_renderer {
                 if (in1) rec[nd.child1] = nrec;
                 if (in2) rec[nd.child2] = nrec + 1;
                 if (in1 || in2) nrec += 2;
-                if (in2) todo.push_back(nd.child2);   // child1's subtree first (depth-first)
-                if (in1) todo.push_back(nd.child1);
+                if (in2) todo.push_back({nd.child2, depth + 1});   // child1's subtree first (depth-first)
+                if (in1) todo.push_back({nd.child1, depth + 1});
             }
         }
         std::vector<int2> big_h;
@@ -1239,11 +1247,10 @@ struct rt_renderer {
         int cur = 0;
         if (n == 0) {                           // a tile owner with no stripe of this image
             // empty event pairs keep the stats bookkeeping aligned: (process) per bounce, (reorder) between
-            for (int k = 0; pass_events && k < 2 * bounces - 1; k++) {
-                hipEvent_t e0 = c.event(), e1 = c.event();
-                if (!e0 || !e1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
-                HIPCHK(hipEventRecord(e0, st));
-                HIPCHK(hipEventRecord(e1, st));
+            for (int k = 0; pass_events && k < 3 * bounces + 2 * (bounces - 1); k++) {
+                hipEvent_t e = c.event();
+                if (!e) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
+                HIPCHK(hipEventRecord(e, st));
             }
             HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
             return RT_OK;
@@ -1256,10 +1263,11 @@ struct rt_renderer {
                           map};
         for (int b = 0; b < bounces; b++) {
             const uint32_t seed_term = 279220567u * (uint32_t)(remaining * 20 + b);
-            hipEvent_t e0 = nullptr, e1 = nullptr;
+            // events per bounce: (process begin, trace end, process end), then (reorder begin, end)
+            hipEvent_t e0 = nullptr, em = nullptr, e1 = nullptr;
             if (pass_events) {
-                e0 = c.event(); e1 = c.event();
-                if (!e0 || !e1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
+                e0 = c.event(); em = c.event(); e1 = c.event();
+                if (!e0 || !em || !e1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
                 HIPCHK(hipEventRecord(e0, st));
             }
             const uint32_t *lv = c.live.p + b;
@@ -1270,6 +1278,7 @@ struct rt_renderer {
         if (!inline_hits)                                                                                        \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
                                c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                               \
+        if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
                                ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,  \
@@ -1414,7 +1423,8 @@ struct rt_renderer {
 
     // Passes pass_begin + k*stride, k < count, nctx at a time on separate streams; the
     // framebuffer adds stay in pass order through cross-stream events.
-    int run(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st) {
+    // pitch: floats between consecutive passes' sums in pass_sums (0 = W*H*3)
+    int run(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st, size_t pitch = 0) {
         const auto w0 = std::chrono::high_resolution_clock::now();
         HIPCHK(hipSetDevice(device));
         if (stride < 1) stride = 1;
@@ -1440,7 +1450,7 @@ struct rt_renderer {
         for (int k = 0; k < count; k++) {
             PassCtx &c = ctx[k % inflight];
             const int p = pass_begin + k * stride;
-            float *sums = pass_sums ? pass_sums + (size_t)k * px3 : c.psum.p;
+            float *sums = pass_sums ? pass_sums + (size_t)k * (pitch ? pitch : (size_t)px3) : c.psum.p;
             const int rc = enqueue_pass(c, p, sums, sorted);
             if (rc) return rc;
             if (prev_fb) HIPCHK(hipStreamWaitEvent(c.stream, prev_fb, 0));
@@ -1485,17 +1495,21 @@ struct rt_renderer {
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, t_begin, t_end));
             st->kernel_ms = ms;
-            // Per context, events come in (process begin, end) pairs with (reorder begin, end)
-            // pairs between them, in enqueue order.
-            double proc = 0, srt = 0;
+            // Per context, events come in (process begin, trace end, process end) triples with
+            // (reorder begin, end) pairs between them, in enqueue order.
+            double proc = 0, srt = 0, trc = 0;
+            uint64_t trace_launches = 0;
             for (int q = 0; pass_events && q < inflight; q++) {
                 const int passes_here = count > q ? (count - q + inflight - 1) / inflight : 0;
                 size_t e = 0;
                 for (int r = 0; r < passes_here; r++)
                     for (int b = 0; b < bounces; b++) {
-                        HIPCHK(hipEventElapsedTime(&ms, ctx[q].events[e], ctx[q].events[e + 1]));
+                        HIPCHK(hipEventElapsedTime(&ms, ctx[q].events[e], ctx[q].events[e + 2]));
                         proc += ms;
-                        e += 2;
+                        HIPCHK(hipEventElapsedTime(&ms, ctx[q].events[e], ctx[q].events[e + 1]));
+                        trc += ms;
+                        trace_launches += inline_hits ? 0 : 1;
+                        e += 3;
                         if (b + 1 != bounces) {     // reorder pair (sort off: the live-ray compaction)
                             HIPCHK(hipEventElapsedTime(&ms, ctx[q].events[e], ctx[q].events[e + 1]));
                             srt += ms;
@@ -1505,6 +1519,8 @@ struct rt_renderer {
             }
             st->process_ms = proc;
             st->sort_ms = srt;
+            st->trace_ms = inline_hits ? 0.0 : trc;
+            st->trace_launches = trace_launches;
             st->generated_rays = (uint64_t)generated;
             st->live_segments = c.live;
             st->sorted_items = (uint64_t)sorted;
@@ -1605,6 +1621,12 @@ int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer *
     return RT_OK;
 }
 
+int rtamd_renderer_run_pitched(rt_renderer *r, int pass_begin, int count, int stride, float *d_pass_sums,
+                               size_t pitch, rt_stats *stats) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    return r->run(pass_begin, count, stride, d_pass_sums, stats, pitch);
+}
+
 int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride, float *d_pass_sums,
                     rt_stats *stats) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
@@ -1672,6 +1694,10 @@ int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stat
     if (!fb_out) return rtamd::fail(RT_E_INVALID, "null framebuffer");
     rt_opts o;
     if (opts) o = *opts; else rt_default_opts(&o);
+    if (o.device_count >= 1) {         // multi-GPU pass sharding over RCCL (rt_multi.hip)
+        const int rc = check_scene(scene);
+        return rc ? rc : rtamd_render_multi(scene, &o, fb_out, stats);
+    }
     rt_renderer *r = nullptr;
     int rc = rt_renderer_create(scene, &o, &r);
     if (rc) return rc;

@@ -8,8 +8,9 @@
 // specified" + exit 2 for no_gpu without cpu, unknown words ignored, asset paths relative to
 // the CWD, the same stdout lines, CPU image stacked above the GPU image, output
 // raytracing.png.  Added: the --options above (all optional).  --devices N renders whole
-// 20-spp passes round-robin on N GPUs (one host thread each) and sums the per-pass
-// framebuffers in pass order, so the image is identical to the 1-GPU image.
+// 20-spp passes round-robin on GPUs 0..N-1 inside the library (rt_opts.device_count: one
+// RCCL communicator, pass-sum slices exchanged over xGMI and added in pass order by their
+// owner, then gathered to GPU 0), so the image is identical to the 1-GPU image.
 #include "rt_abi.h"
 
 #include <algorithm>
@@ -28,55 +29,6 @@ int die(const char *what) {
     return 1;
 }
 
-struct DeviceResult {
-    int rc = 0;
-    std::string err;
-    std::vector<float> sums;   // [passes on this device][W*H*3]
-    rt_stats stats{};
-};
-
-// Multi-GPU pass sharding: device k renders passes k, k+N, ...; pass sums come back to the
-// host and are added in pass order (bit-identical to one device).
-int render_multi(const rt_scene *s, int sort, int ndev, std::vector<float> &fb, rt_stats *total) {
-    const int P = (s->ray_count + 19) / 20;
-    const size_t px3 = (size_t)s->width * s->height * 3;
-    std::vector<DeviceResult> res(ndev);
-    std::vector<std::thread> th;
-    for (int k = 0; k < ndev; k++) {
-        th.emplace_back([&, k]() {
-            DeviceResult &r = res[k];
-            const int count = k < P ? (P - k + ndev - 1) / ndev : 0;
-            if (!count) return;
-            rt_opts o;
-            rt_default_opts(&o);
-            o.sort = sort;
-            o.device = k;
-            rt_renderer *ren = nullptr;
-            r.rc = rt_renderer_create(s, &o, &ren);
-            if (r.rc) { r.err = rt_last_error(); return; }
-            // All of this device's passes in one call (several in flight), sums back to the host.
-            r.sums.assign((size_t)count * px3, 0.0f);
-            r.rc = rt_renderer_run_host(ren, k, count, ndev, r.sums.data(), &r.stats);
-            if (r.rc) r.err = rt_last_error();
-            rt_renderer_destroy(ren);
-        });
-    }
-    for (auto &t : th) t.join();
-    for (auto &r : res)
-        if (r.rc) { std::printf("Error rt_renderer %s\n", r.err.c_str()); return r.rc; }
-    fb.assign(px3, 0.0f);
-    for (int p = 0; p < P; p++) {
-        const float *src = res[p % ndev].sums.data() + (size_t)(p / ndev) * px3;
-        for (size_t i = 0; i < px3; i++) fb[i] = fb[i] + src[i];
-    }
-    for (auto &r : res) {
-        total->live_segments += r.stats.live_segments;
-        total->generated_rays += r.stats.generated_rays;
-        total->kernel_ms = std::max(total->kernel_ms, r.stats.kernel_ms);
-    }
-    return 0;
-}
-
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -88,7 +40,7 @@ int main(int argc, char **argv) {
         return 1;
     }
     bool sort = true, cpu = false, gpu = true, bvh = true, gpu_bvh = false;
-    int devices = 1, device = 0;
+    int devices = 0, device = 0;          // devices 0: not given (the single device `device`)
     const char *asset_root = nullptr, *out_path = "raytracing.png", *stats_path = nullptr;
     rt_load_opts lo;
     rt_default_load_opts(&lo);
@@ -127,7 +79,7 @@ int main(int argc, char **argv) {
     } warm;
     if (gpu)
         warm.t = std::thread([=] {
-            for (int k = 0; k < (devices > 1 ? devices : 1); k++) (void)rt_device_warmup(devices > 1 ? k : device);
+            for (int k = 0; k < (devices > 0 ? devices : 1); k++) (void)rt_device_warmup(devices > 0 ? k : device);
         });
     lo.use_bvh = bvh ? 1 : 0;
     lo.asset_root = asset_root;
@@ -150,15 +102,12 @@ int main(int argc, char **argv) {
     if (gpu) {
         const auto g0 = std::chrono::high_resolution_clock::now();
         if (warm.t.joinable()) warm.t.join();
-        if (devices > 1) {
-            if (render_multi(s, sort ? 1 : 0, devices, fb, &gst)) return 1;
-        } else {
-            rt_opts o;
-            rt_default_opts(&o);
-            o.sort = sort ? 1 : 0;
-            o.device = device;
-            if (rt_render(s, &o, fb.data(), &gst)) return die("gpu_raytrace");
-        }
+        rt_opts o;
+        rt_default_opts(&o);
+        o.sort = sort ? 1 : 0;
+        o.device = device;
+        if (devices > 0) o.device_count = devices;   // devices 0..N-1, RCCL inside rt_render
+        if (rt_render(s, &o, fb.data(), &gst)) return die("gpu_raytrace");
         std::printf("GPU Took %gs\n",
                     std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - g0).count());
         if (rt_bloom(fb.data(), s->width, s->height, (float)(0.7 * s->ray_count), 5, device)) return die("bloom");
@@ -175,7 +124,7 @@ int main(int argc, char **argv) {
                          "\"sort\": %d, \"devices\": %d, \"render_ms\": %.3f, \"kernel_ms\": %.3f, "
                          "\"live_segments\": %llu, \"generated_rays\": %llu, \"live_mrays_per_s\": %.3f, "
                          "\"cpu_s\": %.6f, \"bvh_ms\": %.3f}\n",
-                         argv[1], s->width, s->height, s->ray_count, s->bounces, sort ? 1 : 0, devices, gst.render_ms,
+                         argv[1], s->width, s->height, s->ray_count, s->bounces, sort ? 1 : 0, devices > 0 ? devices : 1, gst.render_ms,
                          gst.kernel_ms, (unsigned long long)gst.live_segments, (unsigned long long)gst.generated_rays,
                          secs > 0 ? gst.live_segments / secs / 1e6 : 0.0, cpu_s, rt_scene_bvh_ms(host));
             std::fclose(f);

@@ -57,7 +57,8 @@ class RtLoadOpts(C.Structure):
 class RtOpts(C.Structure):
     _fields_ = [("sort", I32), ("device", I32), ("pass_begin", I32), ("pass_count", I32),
                 ("pass_stride", I32), ("collect_counters", I32),
-                ("tile_count", I32), ("tile_index", I32), ("tile_rows", I32)]
+                ("tile_count", I32), ("tile_index", I32), ("tile_rows", I32),
+                ("device_count", I32), ("device_ids", C.POINTER(I32))]
 
 
 class RtStats(C.Structure):
@@ -66,7 +67,8 @@ class RtStats(C.Structure):
                                           "sphere_tests", "hits", "misses", "hits_sphere",
                                           "dead_slots")] + \
                [("passes", C.c_uint32), ("reserved", C.c_uint32)] + \
-               [(n, C.c_double) for n in ("render_ms", "kernel_ms", "process_ms", "sort_ms")]
+               [(n, C.c_double) for n in ("render_ms", "kernel_ms", "process_ms", "sort_ms", "trace_ms")] + \
+               [("trace_launches", C.c_uint64), ("exchange_ms", C.c_double)]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if t is C.c_double else int(getattr(self, n)))
@@ -236,11 +238,18 @@ def tile_rows_of(height, tile_count, tile_index, tile_rows=8):
 
 
 def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=1, counters=False,
-           tiles=None):
-    """rt_render: the drop-in for gpu_raytrace.  Returns (framebuffer W*H*3 float32, stats)."""
+           tiles=None, devices=None):
+    """rt_render: the drop-in for gpu_raytrace.  Returns (framebuffer W*H*3 float32, stats).
+    devices = list of device ordinals: the in-library multi-GPU render (pass sharding + RCCL
+    slice exchange and gather; rt_opts.device_count/device_ids), also at one device."""
     fb = np.zeros(scene.pixels * 3, np.float32)
     st = RtStats()
     o = default_opts(sort, device, pass_begin, pass_count, pass_stride, counters, tiles)
+    ids = None
+    if devices is not None:
+        ids = (I32 * len(devices))(*[int(d) for d in devices])
+        o.device_count = len(devices)
+        o.device_ids = C.cast(ids, C.POINTER(I32))
     _check(lib().rt_render(scene.ptr, C.byref(o), _ptr(fb), C.byref(st)))
     return fb, st.as_dict()
 

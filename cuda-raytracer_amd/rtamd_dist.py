@@ -63,6 +63,10 @@ class PassShardedFrame:
         self.slice.zero_()
         self.fb = None
 
+    def _sync(self):
+        if getattr(self.buf, "is_cuda", False):
+            self.torch.cuda.current_stream().synchronize()
+
     def run_rounds(self, k0: int, nrounds: int) -> int:
         """Rounds k0 .. k0+nrounds-1: rank r renders passes r + N*k (those that exist) in one
         renderer call per chunk; the pass slices go to their owners, which add them in pass
@@ -74,6 +78,10 @@ class PassShardedFrame:
             m = len(ks)
             mine = [self.rank + N * k for k in ks if self.rank + N * k < self.passes]
             if mine:
+                # The renderer writes the pass sums on its own streams, which do not wait for torch's:
+                # torch work queued earlier that still reads these buffers (the last chunk's
+                # all_to_all send copy, the stage -> buf copy) must finish first.
+                self._sync()
                 if self.stage is None:
                     self.render_passes(mine, self.buf[:len(mine)])
                 else:
@@ -148,6 +156,10 @@ class TileShardedFrame:
         self.fb: Optional[object] = None
 
     def render(self):
+        # the renderer's streams do not wait for torch's: the last collect's index_select of
+        # `local` must have read it before the renderer overwrites it
+        if getattr(self.local, "is_cuda", False):
+            self.torch.cuda.current_stream().synchronize()
         self.render_tile(self.local)
 
     def collect(self):

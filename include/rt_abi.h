@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum {
     RT_OK = 0,
@@ -109,6 +109,15 @@ typedef struct {
     int32_t tile_count;
     int32_t tile_index;
     int32_t tile_rows;    /* stripe height in rows; 0 = 8 */
+    /* Multi-GPU in one process (rt_render only): device_count > 1 renders whole
+     * passes round-robin over device_ids[0..device_count) (NULL = devices 0..device_count-1), one
+     * host thread and renderer per device, in one RCCL communicator (ncclCommInitAll).  Pass
+     * framebuffers are exchanged as pixel slices (ncclAllToAll over xGMI: slice j goes to device
+     * j, which adds the slices in pass order, bit-identical to one device) and the finished
+     * slices are gathered to device_ids[0] (ncclGather), then copied to fb_out.  0 or 1 = the
+     * single device `device`.  The reference ran one device (raytracing.cu:170-284). */
+    int32_t device_count;
+    const int32_t *device_ids;
 } rt_opts;
 
 typedef struct {
@@ -127,6 +136,11 @@ typedef struct {
     double kernel_ms;          /* HIP-event time of the whole pass loop on the stream      */
     double process_ms;         /* HIP-event time summed over the process (traversal) launches */
     double sort_ms;            /* HIP-event time summed over the reorder launches          */
+    double trace_ms;           /* HIP-event time summed over the trace_kernel launches (a subset
+                                  of process_ms; 0 for scenes without triangles, which have none) */
+    uint64_t trace_launches;   /* trace_kernel launches timed in trace_ms                  */
+    double exchange_ms;        /* multi-GPU rt_render: host wall time of the RCCL slice exchange
+                                  and gather (max over devices)                            */
 } rt_stats;
 
 void rt_default_opts(rt_opts *opts);

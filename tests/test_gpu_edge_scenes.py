@@ -76,3 +76,33 @@ def test_edge_scene_render_bitexact(paths, name, sort):
     assert np.array_equal(gfb, ofb)
     assert gst["live_segments"] == ost["live_segments"]
     assert gst["nodes_popped"] == ost["nodes_popped"]
+
+
+def test_bvh_deeper_than_the_stack_is_refused(paths):
+    """A caller-supplied BVH (rt_scene.bvh, e.g. through the reference-side binding of
+    INTEGRATION.md) deeper than the trace kernel's 32-entry stack is refused with RT_E_INVALID
+    instead of running past the per-lane overflow stack.  The loader caps depth at the
+    reference's MAX_BVH_DEPTH 30 (scene.cu:10), so the chain is built by hand: internal node
+    2k+1 has children (2k+3, 2k+4), 2k+4 an empty leaf."""
+    import ctypes as C
+    psc = R.Scene(paths["deep"])
+    for levels, ok in ((31, True), (40, False)):
+        nodes = np.zeros((2 * levels + 1, 8), np.float32)
+        ints = nodes.view(np.int32)
+        nodes[:, 0:3], nodes[:, 3:6] = -1e30, 1e30
+        ints[0, 6:8] = (1, 2)                       # root: children 1 (internal), 2 (empty leaf)
+        for k in range(levels - 1):
+            ints[2 * k + 1, 6:8] = (2 * k + 3, 2 * k + 4)
+        # leaves: child2 <= child1 (empty: 0, 0); the deepest internal node's children are leaves
+        v = psc.view
+        saved = (v.bvh, v.bvh_node_count)
+        v.bvh, v.bvh_node_count = nodes.ctypes.data, nodes.shape[0]
+        try:
+            rays = np.array([[0, 0, 0, 1, 0, 0]], np.float32)
+            if ok:
+                R.trace_rays(psc, rays)
+            else:
+                with pytest.raises(R.RtError, match="deeper"):
+                    R.trace_rays(psc, rays)
+        finally:
+            v.bvh, v.bvh_node_count = saved

@@ -115,8 +115,9 @@ def test_cli_gpu_png_matches_oracle(gpu, tmp_path):
 
 
 def test_cli_multi_device_equals_single(gpu, tmp_path):
-    """--devices N pass sharding (host threads) gives the 1-device image; with one GPU on the
-    box N=1 is the only runnable case, so this checks the --devices plumbing at N=1."""
+    """--devices N (the in-library RCCL pass sharding, rt_opts.device_count) gives the 1-device
+    image; with one GPU on the box N=1 is the only runnable case: the RCCL communicator, the
+    slice all-to-all, the owner's ordered adds and the gather all run with one rank."""
     import subprocess
     args = ["cornell.scene", "--image", "48", "48", "60", "4", "1"]
     a = subprocess.run([R.CLI_PATH] + args + ["--out", str(tmp_path / "a.png")], cwd=R.ASSETS, capture_output=True)
@@ -162,3 +163,29 @@ def test_fused_and_plain_reorder_bitexact(gpu, monkeypatch, scene, image, sort, 
     assert np.array_equal(gfb, ofb), _diff(gfb, ofb)
     assert gst["live_segments"] == ost["live_segments"]
     assert gst["hits"] == ost["hits_triangle"] + ost["hits_sphere"] and gst["misses"] == ost["misses"]
+
+
+@pytest.mark.parametrize("scene,image,sort", [("cornell_plus", (40, 32, 350, 5), True),    # 18 passes: two chunks
+                                              ("cornell", (33, 17, 190, 4), False),        # 10 passes, odd size
+                                              ("teapot", (64, 36, 45, 16), True)])         # short last pass
+def test_multi_device_rccl_bitexact(gpu, scene, image, sort):
+    """rt_render with rt_opts.device_count (in-library pass sharding over an RCCL communicator,
+    slice all-to-all, ordered owner adds, gather to the first device) at N = 1, the only device
+    count this box has: bit-exact against the oracle and the single-device render."""
+    osc, psc = _pair(scene, image)
+    ofb, ost = osc.render(sort=sort)
+    gfb, gst = R.render(psc, sort=sort, devices=[0])
+    assert np.array_equal(gfb, ofb), _diff(gfb, ofb)
+    assert gst["live_segments"] == ost["live_segments"]
+    assert gst["passes"] == psc.passes
+    assert gst["exchange_ms"] > 0
+
+
+def test_multi_device_rejects_bad_device_lists(gpu):
+    _, psc = _pair("cornell", (16, 16, 20, 2))
+    with pytest.raises(R.RtError, match="twice"):
+        R.render(psc, devices=[0, 0])
+    with pytest.raises(R.RtError, match="no such"):
+        R.render(psc, devices=[0, R.device_count()])
+    with pytest.raises(R.RtError, match="whole frame"):
+        R.render(psc, devices=[0], pass_begin=1)

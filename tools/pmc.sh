@@ -5,7 +5,8 @@
 TAG=$1; GROUPS_FILE=$2; shift 2
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-BENCH="python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-counters $*"
+# exactly one rendered pass: --no-extras skips the event, counter, full-frame and parity legs
+BENCH="python3 bench.py --steps 1 --warmup 0 --no-extras $*"
 i=0
 while read -r GROUP; do
   [ -z "$GROUP" ] && continue

@@ -1,7 +1,7 @@
 """Summarise tools/pmc.sh output per kernel: every collected counter averaged per dispatch, plus
 derived figures (HBM-side bytes, L2 hit rate, VALU utilisation, TA busy).
 
-    python tools/pmc_summary.py TAG [TAG ...] [--json out.json --workload "..." --bounces 16]
+    python tools/pmc_summary.py TAG [TAG ...] [--json profiles/pmc_traffic.json --workload "..." --run "..."]
 
 HBM-side bytes: FETCH_SIZE/WRITE_SIZE as reported, and the request-size-priced figure
 128*RDREQ_128B + 64*RDREQ_64B + 32*RDREQ_32B (MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE
@@ -77,7 +77,7 @@ def derive(avg):
 def main():
     argv = sys.argv[1:]
     opts = {}
-    for flag in ("--json", "--workload", "--bounces"):
+    for flag in ("--json", "--workload", "--run"):
         if flag in argv:
             i = argv.index(flag)
             opts[flag] = argv[i + 1]
@@ -94,25 +94,42 @@ def main():
         summary[k] = rec
         print("%-30s n=%3d %s" % (k, len(ds), "  ".join("%s=%.4g" % kv for kv in sorted(rec["derived"].items()))))
     if "--json" in opts:
-        bounces = int(opts.get("--bounces", 16))
-        rec = {"workload": opts.get("--workload", ""), "source": "rocprofv3 --pmc, one pass per counter group "
-               "(tools/pmc.sh; tags %s)" % ",".join(argv), "kernels": summary}
-        proc = [k for k in summary if k.startswith("trace_kernel") or k.startswith("shade_kernel")]
+        # profiles/pmc_traffic.json: {workload: record}; bench.py reads the record of its workload
+        path = opts["--json"]
+        try:
+            allrec = json.load(open(path))
+        except (OSError, ValueError):
+            allrec = {}
+        passes = summary.get("fill_live_kernel", {}).get("dispatches", 0)   # one per rendered pass
+        trace = [k for k in summary if k.startswith("trace_kernel")]
 
-        def total(field):
-            return sum(summary[k]["derived"].get(field, 0) * summary[k]["dispatches"] for k in proc)
-        rd = total("read_bytes_by_size") or total("fetch_size_bytes")
-        wr = total("write_bytes_by_size") or total("write_size_bytes")
-        if proc and rd:
-            rec["hbm_bytes_per_launch"] = int((rd + wr) / bounces)
-            rec["hbm_read_bytes_per_launch"] = int(rd / bounces)
-            rec["hbm_write_bytes_per_launch"] = int(wr / bounces)
-            rec["fetch_size_bytes_per_launch"] = int(total("fetch_size_bytes") / bounces)
-            rec["note"] = ("per process launch = one trace_kernel + one shade_kernel dispatch (bounce 0 included), "
-                           "summed over the bounces of the profiled pass and divided by their number; reads priced by "
-                           "request size (TCC_EA0_RDREQ_{128B,64B,32B}), writes by TCC_EA0_WRREQ{,_64B}; L2->fabric "
-                           "requests, so Infinity-Cache hits are included (an upper bound on HBM bytes)")
-        json.dump(rec, open(opts["--json"], "w"), indent=1)
+        def total(keys, field):
+            return sum(summary[k]["derived"].get(field, 0) * summary[k]["dispatches"] for k in keys)
+
+        def hbm(keys):
+            rd = total(keys, "read_bytes_by_size") or 2 * total(keys, "fetch_size_bytes")
+            wr = total(keys, "write_bytes_by_size") or total(keys, "write_size_bytes")
+            return rd, wr
+        rec = {"source": "rocprofv3 --pmc, one invocation per counter group (tools/pmc.sh; tags %s)" % ",".join(argv),
+               "run": opts.get("--run", ""), "passes_profiled": passes, "kernels": summary}
+        n_trace = sum(summary[k]["dispatches"] for k in trace)
+        if passes and n_trace:
+            rd, wr = hbm(trace)
+            rec["trace_launches"] = n_trace
+            rec["trace_bytes_per_launch"] = int((rd + wr) / n_trace)
+            rec["trace_read_bytes_per_launch"] = int(rd / n_trace)
+            rec["trace_write_bytes_per_launch"] = int(wr / n_trace)
+            rec["trace_fetch_size_bytes_per_launch"] = int(total(trace, "fetch_size_bytes") / n_trace)
+            rd, wr = hbm(list(summary))
+            rec["pass_bytes"] = int((rd + wr) / passes)
+            rec["note"] = ("trace_bytes_per_launch: summed over every trace_kernel dispatch of the profiled passes and "
+                           "divided by their number; pass_bytes: every kernel's bytes divided by the passes profiled "
+                           "(fill_live_kernel dispatches).  Reads priced by request size (TCC_EA0_RDREQ_{128B,64B,32B}; "
+                           "2 x FETCH_SIZE where those are missing, MI355X_MICROARCH.md §HBM), writes by "
+                           "TCC_EA0_WRREQ{,_64B}; L2->fabric requests, so Infinity-Cache hits are included (an upper "
+                           "bound on HBM bytes).  The profiler serialises dispatches.")
+        allrec[opts.get("--workload", "")] = rec
+        json.dump(allrec, open(path, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
