@@ -359,9 +359,10 @@ def main():
                     "bytes_per_launch": int(comp), "ms_per_launch": round(trace_ms, 4), "launches": launches,
                     "achieved_def": "algorithmic HBM bytes per trace launch (24 B ray read per live segment past "
                                     "bounce 0 + 8 B hit write per live segment + the scene's node/triangle arrays "
-                                    "once, reference layouts) / average trace launch duration (HIP events on the "
-                                    "pass's stream, untimed re-run of the timed steps; up to 20 passes share the chip, "
-                                    "so a launch's duration includes time it shared)",
+                                    "once, reference layouts) / average trace launch duration (device wall clock from "
+                                    "the launch's first wave start to its last wave end, read in an untimed re-run of "
+                                    "the timed steps; up to 20 passes share the chip, so a launch's duration includes "
+                                    "time it shared, as in rocprofv3's kernel trace)",
                     "traffic_def": None if not pmc else
                     "measured HBM-side bytes per trace launch, rocprofv3 --pmc, one profiled pass "
                     "(%s; reads priced by request size TCC_EA0_RDREQ_{128B,64B,32B}, = 2 x FETCH_SIZE for 128-B "

@@ -256,8 +256,13 @@ template <bool SORTED, bool COUNT, int FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
-                                                       uint32_t *__restrict__ overflow, Counters *__restrict__ ctr) {
+                                                       uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
+                                                       unsigned long long *__restrict__ tspan) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
+    // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
+    // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
+    // before its first wave and the stream's marker packets (what rocprofv3 reports)
+    if (tspan && lane_id() == 0) atomicMin(&tspan[0], (unsigned long long)wall_clock64());
     uint2 *col = stack + threadIdx.x;
     // Overflow tail of the stack (entries >= kStackLds, rare) in a global per-lane buffer,
     // [entry][lane] for coalescing; refs and distances in two 32-bit halves so the compiler cannot
@@ -473,6 +478,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         }
     }
     if (lane_id() == 0 && nl) atomicAdd(&cs->live, nl);
+    if (tspan && lane_id() == 0) atomicMax(&tspan[1], (unsigned long long)wall_clock64());
 #ifdef RT_PROFILE
     prof[11] = wave_sum((unsigned)prof[10]);   // pop iterations summed over the lanes
     if (lane_id() == 0)
@@ -611,10 +617,13 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
     }
 }
 
-__global__ void fill_live_kernel(uint32_t *__restrict__ live, uint32_t n, int count, uint32_t *__restrict__ queue) {
+__global__ void fill_live_kernel(uint32_t *__restrict__ live, uint32_t n, int count, uint32_t *__restrict__ queue,
+                                 unsigned long long *__restrict__ tspan) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) live[i] = n;
     for (int k = i; k < count * kQueues * kQueueStride; k += blockDim.x) queue[k] = 0;
+    if (tspan)
+        for (int k = i; k < 2 * count; k += blockDim.x) tspan[k] = (k & 1) ? 0ull : ~0ull;
 }
 
 
@@ -1023,6 +1032,8 @@ struct rt_renderer {
     DevBuf<int2> big;
     DevBuf<float> env, fb;
     DevBuf<Counters> ctr;
+    DevBuf<unsigned long long> tspans;   // per run: [pass][bounce] trace-launch wall-clock spans (event timing on)
+    int wall_khz = 0;                    // device wall clock rate (wall_clock64 ticks per ms)
     PassCtx ctx[kInflight];
     int trace_blocks = 0;             // persistent trace_kernel grid of the current run
     int trace_blocks_max = 0;         // all resident trace workgroups (the overflow stacks are sized for it)
@@ -1229,7 +1240,8 @@ struct rt_renderer {
 
     // Pass p of `while (remaining_rays)` (raytracing.cu:222-254) on context c; the pass's
     // per-pixel sums go to `sums` (W*H*3).
-    int enqueue_pass(PassCtx &c, int p, float *sums, int64_t &sorted) {
+    // tspan: 2 * (bounces + 1) words for this pass's trace-launch wall-clock spans, or null
+    int enqueue_pass(PassCtx &c, int p, float *sums, int64_t &sorted, unsigned long long *tspan) {
         const int before = spp - 20 * p;
         const int rtc = std::min(before, 20);
         const int remaining = before - rtc;
@@ -1255,7 +1267,7 @@ struct rt_renderer {
             HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
             return RT_OK;
         }
-        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1, c.queue.p);
+        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, st, c.live.p, (uint32_t)n, bounces + 1, c.queue.p, tspan);
         const uint32_t stripe_px = (uint32_t)(tile_rows * width);
         const SlotMap pix = tiled() ? SlotMap::of(stripe_px, tile_count, tile_index) : SlotMap::identity();
         const SlotMap map = tiled() ? SlotMap::of(stripe_px * (uint32_t)rtc, tile_count, tile_index) : SlotMap::identity();
@@ -1277,7 +1289,7 @@ struct rt_renderer {
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p);                               \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + 2 * b : nullptr); \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
@@ -1397,10 +1409,10 @@ struct rt_renderer {
         const int tgrid = std::min(blocks_for(n), trace_blocks);
         if (counters)
             hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               live.p, queue.p, hits.p, overflow.p, ctr.p);
+                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr);
         else
             hipLaunchKernelGGL((trace_kernel<false, false, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               live.p, queue.p, hits.p, overflow.p, ctr.p);
+                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr);
         HIPCHK(hipGetLastError());
         std::vector<float2> h((size_t)n);
         HIPCHK(hipMemcpyAsync(h.data(), hits.p, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, s0));
@@ -1440,6 +1452,10 @@ struct rt_renderer {
             trace_blocks = std::max(1, trace_blocks_max * pct / 100);
         }
         hipStream_t s0 = stream();
+        if (pass_events && tspans.n < (size_t)std::max(count, 1) * 2 * (bounces + 1)) {
+            if (int rc = tspans.alloc((size_t)std::max(count, 1) * 2 * (bounces + 1))) return rc;
+            if (!wall_khz) HIPCHK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, device));
+        }
         HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, s0));
         HIPCHK(hipEventRecord(t_begin, s0));
         for (int k = 1; k < inflight; k++) HIPCHK(hipStreamWaitEvent(ctx[k].stream, t_begin, 0));
@@ -1451,7 +1467,8 @@ struct rt_renderer {
             PassCtx &c = ctx[k % inflight];
             const int p = pass_begin + k * stride;
             float *sums = pass_sums ? pass_sums + (size_t)k * (pitch ? pitch : (size_t)px3) : c.psum.p;
-            const int rc = enqueue_pass(c, p, sums, sorted);
+            const int rc = enqueue_pass(c, p, sums, sorted,
+                                        pass_events ? tspans.p + (size_t)k * 2 * (bounces + 1) : nullptr);
             if (rc) return rc;
             if (prev_fb) HIPCHK(hipStreamWaitEvent(c.stream, prev_fb, 0));
             hipLaunchKernelGGL(add_kernel, dim3(blocks_for(px3)), dim3(kBlock), 0, c.stream, fb.p, sums, (int)px3);
@@ -1506,14 +1523,26 @@ struct rt_renderer {
                     for (int b = 0; b < bounces; b++) {
                         HIPCHK(hipEventElapsedTime(&ms, ctx[q].events[e], ctx[q].events[e + 2]));
                         proc += ms;
-                        HIPCHK(hipEventElapsedTime(&ms, ctx[q].events[e], ctx[q].events[e + 1]));
-                        trc += ms;
-                        trace_launches += inline_hits ? 0 : 1;
                         e += 3;
                         if (b + 1 != bounces) {     // reorder pair (sort off: the live-ray compaction)
                             HIPCHK(hipEventElapsedTime(&ms, ctx[q].events[e], ctx[q].events[e + 1]));
                             srt += ms;
                             e += 2;
+                        }
+                    }
+            }
+            // trace launches: the device wall-clock span from the first wave's start to the last
+            // wave's end (the stream's events would add the queueing before the first wave)
+            if (pass_events && !inline_hits && count > 0) {
+                std::vector<unsigned long long> sp((size_t)count * 2 * (bounces + 1));
+                HIPCHK(hipMemcpy(sp.data(), tspans.p, sp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+                for (int k = 0; k < count; k++)
+                    for (int b = 0; b < bounces; b++) {
+                        const unsigned long long t0 = sp[((size_t)k * (bounces + 1) + b) * 2];
+                        const unsigned long long t1 = sp[((size_t)k * (bounces + 1) + b) * 2 + 1];
+                        if (t1 >= t0 && t0 != ~0ull) {
+                            trc += (double)(t1 - t0) / wall_khz;
+                            trace_launches++;
                         }
                     }
             }
@@ -1598,7 +1627,7 @@ int rt_device_warmup(int32_t device) {
     uint32_t *d = nullptr;
     HIPCHK(hipMallocAsync(reinterpret_cast<void **>(&d), 4 * sizeof(uint32_t), s));
     // one (empty: count 0 writes nothing) launch loads this library's code object on the device
-    hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, s, d, 0u, 0, d);
+    hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, s, d, 0u, 0, d, nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipFreeAsync(d, s));
     HIPCHK(hipStreamSynchronize(s));

@@ -136,8 +136,10 @@ typedef struct {
     double kernel_ms;          /* HIP-event time of the whole pass loop on the stream      */
     double process_ms;         /* HIP-event time summed over the process (traversal) launches */
     double sort_ms;            /* HIP-event time summed over the reorder launches          */
-    double trace_ms;           /* HIP-event time summed over the trace_kernel launches (a subset
-                                  of process_ms; 0 for scenes without triangles, which have none) */
+    double trace_ms;           /* trace_kernel launches, summed: each launch's span on the device
+                                  wall clock from its first wave's start to its last wave's end
+                                  (event timing on; 0 for scenes without triangles, which have
+                                  no trace launch)                                          */
     uint64_t trace_launches;   /* trace_kernel launches timed in trace_ms                  */
     double exchange_ms;        /* multi-GPU rt_render: host wall time of the RCCL slice exchange
                                   and gather (max over devices)                            */

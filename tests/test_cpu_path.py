@@ -23,6 +23,20 @@ def test_cpu_path_bitexact(scene, image):
     assert np.array_equal(ofb, pfb)
 
 
+def test_cpu_path_config1_full_size():
+    """BASELINE.json configs[0]: cornell.scene 256x256, 64 spp, 4 bounces through the product's
+    `cpu` path (rt_cpu_render, the drop-in for cpu_raytrace, raytracing.cu:122-163: four passes
+    of 20/20/20/4 rays per pixel, bounce-invariant seed :148), bit-exact against the oracle's
+    restatement at its full size (no GPU needed)."""
+    path = os.path.join(R.ASSETS, "cornell.scene")
+    image = (256, 256, 64, 4)
+    ofb, _ = O.OracleScene(path, image=image).render_cpu_path(threads=8)
+    pfb, secs = R.cpu_render(R.Scene(path, image=image), threads=8)
+    assert np.array_equal(ofb, pfb)
+    assert np.isfinite(pfb).all() and pfb.mean() > 0
+    assert secs > 0
+
+
 def test_tonemap_matches_oracle():
     rng = np.random.default_rng(0)
     fb = (rng.random(300 * 3) * 50).astype(np.float32)
