@@ -9,7 +9,9 @@ now applies: without bloom our means match to 0.006-0.02 levels (block RMS 0.07-
 they are 0.16-1.1 levels brighter everywhere.  So the bloom stage is checked bit-exactly against
 the oracle elsewhere and left out of this statistical comparison.  Bit equality with the PNGs is
 impossible (nvcc --use_fast_math, FMA contraction, unordered float atomics, independent Monte
-Carlo noise); the bounds are ~4x the differences measured.  teapot/lamp/glass_teapot are not
+Carlo noise), so the block comparison is a z-score against the two estimates' own noise (per-block
+pixel noise variance from adjacent pixel pairs), and cornell_plus is also compared on its
+emissive, dielectric and mirror regions alone.  teapot/lamp/glass_teapot are not
 compared: their assets are missing upstream."""
 import json
 import os
@@ -42,8 +44,49 @@ def test_matches_reference_render_statistics(scene):
           "thumb rms %.3f max %.3f" % (np.sqrt((dthumb ** 2).mean()), dthumb.max()),
           "render %.1f ms" % st["render_ms"])
     assert dmean.max() < 0.1
-    assert np.sqrt((dthumb ** 2).mean()) < 1.0
-    assert dthumb.max() < 6.0
+    # Noise-aware block comparison: each 50x50 block mean of two independent 1000-spp estimates
+    # differs by Monte Carlo noise of variance (v_ours + v_ref) / 2500, v = that block's per-pixel
+    # noise variance from adjacent-pixel pairs (tests/golden/make_reference_stats.py)
+    v_ref = np.array(ref["thumb20_noise_var"])
+    v_our = block_noise_var(img)
+    z = (thumb - np.array(ref["thumb20"])) / np.sqrt((v_ref + v_our) / 2500.0 + 1e-12)
+    print(scene, "block z: rms %.2f max %.2f, |z|>3: %d of %d" % (np.sqrt((z ** 2).mean()), np.abs(z).max(),
+                                                                (np.abs(z) > 3).sum(), z.size))
+    assert np.sqrt((z ** 2).mean()) < 1.6
+    assert np.abs(z).max() < 6.0
+    assert (np.abs(z) > 3).sum() <= 0.02 * z.size
     # image noise (adjacent-pixel differences) is that of the reference's 1000-spp estimate
     noise = np.abs(np.diff(img, axis=1)).mean()
     assert abs(noise - ref["adjacent_pixel_absdiff"]) < 0.05 * ref["adjacent_pixel_absdiff"]
+    if scene == "cornell_plus":
+        check_regions(img, ref["regions"])
+
+
+def block_noise_var(img, nb=20):
+    h, w, _ = img.shape
+    d = np.diff(img.reshape(nb, h // nb, nb, w // nb, 3), axis=3)
+    return (d ** 2).mean(axis=(1, 3)) / 2.0
+
+
+def check_regions(img, regions):
+    """cornell_plus's emissive (light quad), dielectric (glass sphere) and mirror regions: pixels
+    whose primary ray first hits them (oracle closest hit, tests/golden/cornell_plus_regions.npz).
+    The glass sphere exercises the dielectric branch (Schlick, TIR, refraction, scene.cu:443-476)
+    and the env-lit caustic paths behind it; the light is pure emission (scene.cu:417)."""
+    packed = np.load(os.path.join(HERE, "golden", "cornell_plus_regions.npz"))
+    for name, rs in regions.items():
+        m = np.unpackbits(packed[name])[:img.shape[0] * img.shape[1]].reshape(img.shape[:2]).astype(bool)
+        assert m.sum() == rs["pixels"]
+        mean = img[m].mean(axis=0)
+        pair = m[:, 1:] & m[:, :-1]
+        d = (img[:, 1:] - img[:, :-1])[pair]
+        v_our = (d ** 2).mean(axis=0) / 2.0
+        delta = mean - np.array(rs["mean"])
+        z = delta / np.sqrt((v_our + np.array(rs["noise_var"])) / rs["pixels"] + 1e-12)
+        print("  region %-10s %6d px  mean %s ref %s  z %s" % (name, rs["pixels"], mean.round(3), rs["mean"], z.round(2)))
+        if name == "emissive":
+            # pure emission: every sample of a covered pixel is exp-mapped 30 -> byte 251; only the
+            # light's edge pixels vary
+            assert np.abs(delta).max() < 0.05
+        else:
+            assert np.abs(z).max() < 5.0, name
