@@ -1620,10 +1620,14 @@ int rt_device_count(void) {
 }
 
 int rt_device_warmup(int32_t device) {
+    InitTimer tm;
     if (device < 0 || device >= rt_device_count()) return rtamd::fail(RT_E_NODEVICE, "no such HIP device");
+    tm.mark("runtime init");
     HIPCHK(hipSetDevice(device));
+    tm.mark("hipSetDevice");
     hipStream_t s;
     HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    tm.mark("stream");
     uint32_t *d = nullptr;
     HIPCHK(hipMallocAsync(reinterpret_cast<void **>(&d), 4 * sizeof(uint32_t), s));
     // one (empty: count 0 writes nothing) launch loads this library's code object on the device
@@ -1631,7 +1635,10 @@ int rt_device_warmup(int32_t device) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipFreeAsync(d, s));
     HIPCHK(hipStreamSynchronize(s));
+    tm.mark("first launch");
     HIPCHK(hipStreamDestroy(s));
+    tm.mark("stream destroy");
+    if (tm.on) std::fprintf(stderr, "rt_device_warmup:%s\n", tm.out.c_str());
     return RT_OK;
 }
 

@@ -73,13 +73,21 @@ int main(int argc, char **argv) {
     // HIP runtime, queue and code-object initialisation (~0.2 s per process) runs on a thread of
     // its own while the scene loads and the BVH builds; the GPU Took span below starts before the
     // wait for it, so whatever is left of it is still counted.
+    const auto t_start = std::chrono::high_resolution_clock::now();
+    auto ms_since = [](std::chrono::high_resolution_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - t).count();
+    };
+    const bool timing = std::getenv("RTAMD_TIMING") != nullptr;
+    double warm_ms = 0;
     struct Warmup {
         std::thread t;
         ~Warmup() { if (t.joinable()) t.join(); }
     } warm;
     if (gpu)
-        warm.t = std::thread([=] {
+        warm.t = std::thread([=, &warm_ms] {
+            const auto w0 = std::chrono::high_resolution_clock::now();
             for (int k = 0; k < (devices > 0 ? devices : 1); k++) (void)rt_device_warmup(devices > 0 ? k : device);
+            warm_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
         });
     lo.use_bvh = bvh ? 1 : 0;
     lo.asset_root = asset_root;
@@ -101,7 +109,11 @@ int main(int argc, char **argv) {
     }
     if (gpu) {
         const auto g0 = std::chrono::high_resolution_clock::now();
+        const double load_ms = ms_since(t_start);
         if (warm.t.joinable()) warm.t.join();
+        if (timing)
+            std::fprintf(stderr, "cli: scene loaded at %.1f ms, HIP warm-up took %.1f ms, waited %.1f ms for it\n", load_ms,
+                         warm_ms, ms_since(g0));
         rt_opts o;
         rt_default_opts(&o);
         o.sort = sort ? 1 : 0;

@@ -12,7 +12,7 @@ for scene in spheres cornell cornell_plus teapot glass_teapot lamp_available; do
   for spp in 1 10 100; do
     for mode in sort no_sort; do
       extra=""; [ $mode = no_sort ] && extra=no_sort
-      line=$(timeout -k 10 120 $BIN $scene.scene $extra --image 1000 1000 $spp 10 1 --out /tmp/t1.png | grep "GPU Took") || { echo "failed: $scene $spp $mode"; exit 1; }
+      line=$(timeout -k 10 120 $BIN $scene.scene $extra --image 1000 1000 $spp 10 1 --out /tmp/t1.png 2>>../$OUT.timing | grep "GPU Took") || { echo "failed: $scene $spp $mode"; exit 1; }
       echo "$scene $spp $mode $(echo $line | awk '{print $3}' | tr -d s)" >> ../$OUT
     done
   done
