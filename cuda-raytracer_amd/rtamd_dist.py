@@ -184,3 +184,17 @@ class TileShardedFrame:
     def run_all(self):
         self.render()
         return self.collect()
+
+
+def bucket_exchange(dist, torch):
+    """The per-bounce exchange of pixel-tile sharding with the reorder on: every
+    owner writes bucket + 1 at the global slot of each of its live rays into a zeroed byte array;
+    the sum over owners (one all-reduce, uint8: each slot has exactly one owner, so no byte
+    exceeds 65) gives every owner the whole bucket array, from which it ranks its own rays.
+    Returns exchange(arr): in-place sum of a numpy uint8 array over the process group."""
+    def exchange(arr):
+        t = torch.from_numpy(arr)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        if t.data_ptr() != arr.ctypes.data:
+            arr[:] = t.numpy()
+    return exchange

@@ -681,21 +681,25 @@ void process_ray(const orc_scene *s, RayData *rp, uint32_t *key, Rng rng, bool g
 }
 
 // ---------------------------------------------------------------- scene.cu:78-105
-void generate_ray(const orc_scene *s, RayData *rays, uint32_t *idx, uint32_t *keys, int rtc, int i, int seed) {
+RayData make_ray(const orc_scene *s, int rtc, int i, int seed) {
     Rng rng;
     xor_srand(&rng, (uint32_t)i * 0x85810BEAu + 709579u * (uint32_t)seed);
     const int fb = i / rtc;
     const int x = fb % s->width, y = fb / s->width;
-    if (y < s->height) {
+    const float xc = (x + random01(&rng)) * s->inv_width;
+    const float yc = (y + random01(&rng)) * s->inv_height;
+    RayData r;
+    r.origin = s->camera_position;
+    r.dir = normalise(s->near_plane_top_left + xc * s->scaled_right - yc * s->scaled_up);
+    r.transmitted = {1, 1, 1};
+    r.collected = {0, 0, 0};
+    return r;
+}
+
+void generate_ray(const orc_scene *s, RayData *rays, uint32_t *idx, uint32_t *keys, int rtc, int i, int seed) {
+    if ((i / rtc) / s->width < s->height) {
         if (idx) { idx[i] = (uint32_t)i; keys[i] = 0; }
-        const float xc = (x + random01(&rng)) * s->inv_width;
-        const float yc = (y + random01(&rng)) * s->inv_height;
-        RayData r;
-        r.origin = s->camera_position;
-        r.dir = normalise(s->near_plane_top_left + xc * s->scaled_right - yc * s->scaled_up);
-        r.transmitted = {1, 1, 1};
-        r.collected = {0, 0, 0};
-        rays[i] = r;
+        rays[i] = make_ray(s, rtc, i, seed);
     }
 }
 
@@ -772,6 +776,100 @@ void gpu_pass(const orc_scene *s, int p, bool sort, float *pass_sum, Counters &t
     }
     total.live += 0;
     (void)n;
+}
+
+// Pixel-tile sharding with the reorder on ("sort on" row) -- the distributed form of
+// gpu_pass that the HIP renderer's tiled sort-on mode implements.  Owner `ti` of `tc` renders only
+// the rays of its row stripes (stripes of `tr` rows dealt round-robin), each with its global ray
+// index i = pixel * rtc + s (so generate seeds are the 1-GPU ones, scene.cu:78-105).  The process
+// seed follows the ray's GLOBAL slot (raytracing.cu:89), which after a sort depends on every
+// owner's keys (raytracing.cu:238-247).  Live rays always occupy global slots [0, Lg), so after
+// each bounce but the last every owner writes bucket + 1 at the global slot of each of its rays
+// into a zeroed byte array of length Lg, `exchange` sums the arrays over the owners (an
+// all-reduce), and every owner ranks its rays exactly as the stable 65-bucket sort of all keys
+// would: new slot = rays in smaller buckets + rays of the same bucket at smaller global slots.
+// Nothing but those bytes crosses owners; rays never migrate.  With sort off the slot is the ray
+// index and no exchange happens.  pass_sum: this owner's pixels only (the rest untouched).
+void tile_pass(const orc_scene *s, int p, bool sort, int tc, int ti, int tr, orc_exchange_fn exchange, void *user,
+               float *pass_sum, Counters &total, int threads) {
+    int rtc, rem;
+    pass_params(s, p, &rtc, &rem);
+    const int W = s->width, H = s->height;
+    std::vector<int64_t> pix;                          // own pixels, ascending (rows of own stripes)
+    for (int k = ti; (int64_t)k * tr < H; k += tc)
+        for (int y = k * tr; y < std::min(H, (k + 1) * tr); y++)
+            for (int x = 0; x < W; x++) pix.push_back((int64_t)y * W + x);
+    const int64_t m = (int64_t)pix.size() * rtc;
+    std::vector<RayData> rays(m);
+    std::vector<uint32_t> keys(m, 0), gslot(m), next(m);
+    const int nt = nthreads(threads);
+    for (int64_t j = 0; j < m; j++) {
+        const int64_t gid = pix[j / rtc] * rtc + j % rtc;
+        gslot[j] = (uint32_t)gid;                      // bounce 0: slot = ray index
+        rays[j] = make_ray(s, rtc, (int)gid, rem);
+    }
+    std::vector<int64_t> live(m);                      // own live rays in global-slot order
+    for (int64_t j = 0; j < m; j++) live[j] = j;
+    int64_t Lg = (int64_t)rtc * W * H;                 // global live count: every generated ray
+    for (int b = 0; b < s->bounces; b++) {
+        const uint32_t seed = (uint32_t)(rem * 20 + b);
+        std::vector<Counters> per(nt);
+#pragma omp parallel num_threads(nt)
+        {
+#ifdef _OPENMP
+            Counters &c = per[omp_get_thread_num()];
+#else
+            Counters &c = per[0];
+#endif
+#pragma omp for schedule(dynamic, 4096)
+            for (int64_t q = 0; q < (int64_t)live.size(); q++) {
+                const int64_t j = live[q];
+                Rng rng;
+                xor_srand(&rng, gslot[j] * 4137874753u + 279220567u * seed);   // raytracing.cu:89
+                process_ray(s, &rays[j], &keys[j], rng, true, c);
+            }
+        }
+        for (auto &c : per) total.add(c);
+        if (b + 1 == s->bounces) break;
+        if (!sort) {                                   // slot = ray index for the whole pass
+            std::vector<int64_t> keep;
+            for (int64_t j : live) if (keys[j] != 0xFFFFFFFFu) keep.push_back(j);
+            live.swap(keep);
+            continue;
+        }
+        std::vector<uint8_t> g((size_t)Lg, 0);
+        for (int64_t j : live) g[gslot[j]] = (uint8_t)(orc_key_bucket(keys[j]) + 1);
+        if (Lg > 0 && exchange(user, g.data(), Lg) != 0) throw std::runtime_error("tile exchange failed");
+        uint64_t cnt[65] = {0};
+        for (int64_t k = 0; k < Lg; k++) {
+            if (g[k] < 1 || g[k] > 65) throw std::runtime_error("tile exchange: a slot has no owner");
+            cnt[g[k] - 1]++;
+        }
+        uint64_t base[65], acc = 0;
+        for (int k = 0; k < 65; k++) { base[k] = acc; acc += cnt[k]; }
+        uint64_t seen[65] = {0};
+        size_t q = 0;                                  // own live rays are in ascending global slot
+        std::vector<int64_t> keep;
+        for (int64_t k = 0; k < Lg; k++) {
+            const int bk = g[k] - 1;
+            if (q < live.size() && (int64_t)gslot[live[q]] == k) {
+                const int64_t j = live[q++];
+                if (bk != 64) { next[j] = (uint32_t)(base[bk] + seen[bk]); keep.push_back(j); }
+            }
+            seen[bk]++;
+        }
+        std::stable_sort(keep.begin(), keep.end(), [&](int64_t a, int64_t c) { return next[a] < next[c]; });
+        for (int64_t j : keep) gslot[j] = next[j];
+        live.swap(keep);
+        Lg -= (int64_t)cnt[64];
+    }
+    for (size_t qp = 0; qp < pix.size(); qp++) {
+        V3 sum{0, 0, 0};
+        for (int k = 0; k < rtc; k++) sum = sum + rays[(int64_t)qp * rtc + k].collected;
+        pass_sum[pix[qp] * 3 + 0] = sum.x;
+        pass_sum[pix[qp] * 3 + 1] = sum.y;
+        pass_sum[pix[qp] * 3 + 2] = sum.z;
+    }
 }
 
 }  // namespace
@@ -859,6 +957,43 @@ int orc_render_gpu_semantics(const orc_scene *s, int sort, int pass_begin, int p
         stats->max_stack = total.max_stack;
         stats->max_ray_nodes = total.max_ray_pn;
         stats->passes = (uint32_t)pass_count;
+    }
+    return 0;
+}
+
+int orc_render_tiled(const orc_scene *s, int sort, int tile_count, int tile_index, int tile_rows, int pass_begin,
+                     int pass_count, orc_exchange_fn exchange, void *user, float *fb, orc_stats *stats, int threads) {
+    const int P = pass_total(s);
+    if (pass_count < 0) pass_count = P - pass_begin;
+    if (pass_begin < 0 || pass_begin + pass_count > P) { g_err = "pass range"; return -1; }
+    if (tile_count < 1 || tile_index < 0 || tile_index >= tile_count || tile_rows < 1 || (sort && !exchange)) {
+        g_err = "bad tile arguments";
+        return -1;
+    }
+    const int64_t pixels = (int64_t)s->width * s->height;
+    std::vector<float> sum(pixels * 3, 0.0f);
+    Counters total;
+    uint64_t generated = 0;
+    try {
+        for (int p = pass_begin; p < pass_begin + pass_count; p++) {
+            tile_pass(s, p, sort != 0, tile_count, tile_index, tile_rows, exchange, user, sum.data(), total, threads);
+            for (int64_t k = 0; k < pixels * 3; k++) fb[k] = fb[k] + sum[k];   // other owners' pixels: + 0
+        }
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->live_segments = total.live;
+        stats->nodes_popped = total.pn;
+        stats->internal_visits = total.iv;
+        stats->triangle_tests = total.tt;
+        stats->hits_triangle = total.ht;
+        stats->hits_sphere = total.hs;
+        stats->misses = total.miss;
+        stats->passes = (uint32_t)pass_count;
+        (void)generated;
     }
     return 0;
 }

@@ -76,6 +76,13 @@ int orc_render_gpu_semantics(const orc_scene *s, int sort, int pass_begin, int p
                              float *fb_inout, orc_stats *stats, uint64_t *bucket_hist,
                              int threads);
 /* Per-pass sums instead of the running framebuffer: out[pass][W*H*3]. */
+/* Pixel-tile sharding with the per-bounce bucket exchange (SURVEY §8e "sort on"): this owner's
+ * stripes only; `exchange` must sum `n` bytes in place over all owners (an all-reduce) and return
+ * 0.  fb_inout += this owner's pass sums, pass by pass (other pixels untouched). */
+typedef int (*orc_exchange_fn)(void *user, uint8_t *bytes, int64_t n);
+int orc_render_tiled(const orc_scene *s, int sort, int tile_count, int tile_index, int tile_rows,
+                     int pass_begin, int pass_count, orc_exchange_fn exchange, void *user,
+                     float *fb_inout, orc_stats *stats, int threads);
 int orc_render_pass_sums(const orc_scene *s, int sort, int pass_begin, int pass_count,
                          float *out, int threads);
 

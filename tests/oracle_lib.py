@@ -32,6 +32,9 @@ class OrcStats(C.Structure):
 _lib = None
 
 
+
+EXCHANGE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_int64)
+
 def build():
     subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
 
@@ -51,6 +54,8 @@ def lib():
         L.orc_get_arrays.argtypes = [P] * 8
         L.orc_render_gpu_semantics.argtypes = [P, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int]
         L.orc_render_pass_sums.argtypes = [P, C.c_int, C.c_int, C.c_int, P, C.c_int]
+        L.orc_render_tiled.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, EXCHANGE, P, P, P,
+                                       C.c_int]
         L.orc_render_cpu_path.argtypes = [P, P, C.c_int, C.c_int, P]
         L.orc_closest_hit.argtypes = [P, P, C.c_int, P, P, P]
         L.orc_bloom.argtypes = [P, C.c_int, C.c_int, C.c_float, C.c_int]
@@ -139,6 +144,27 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(lib().orc_last_error().decode())
         return out
+
+    def render_tiled(self, exchange, tile_count, tile_index, tile_rows=8, sort=True, pass_begin=0, pass_count=-1,
+                     threads=0):
+        """orc_render_tiled: this owner's row stripes only, with the per-bounce bucket exchange
+        (SURVEY §8e sort on).  exchange(arr) must sum the uint8 array over all owners in place.
+        Returns (fb with this owner's pixels, others 0; stats)."""
+        fb = np.zeros(self.pixels * 3, np.float32)
+        st = OrcStats()
+
+        def cb(user, p, n):
+            try:
+                exchange(np.ctypeslib.as_array(p, shape=(n,)))
+                return 0
+            except Exception:       # reported as a failed exchange by the oracle
+                return -1
+        fn = EXCHANGE(cb)
+        rc = lib().orc_render_tiled(self.h, int(sort), tile_count, tile_index, tile_rows, pass_begin, pass_count, fn,
+                                    None, ptr(fb), C.byref(st), threads)
+        if rc != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+        return fb, st.as_dict()
 
     def closest_hit(self, rays):
         """Closest hit of rays (n, 6) {o.xyz, d.xyz}: (t, index, stats)."""

@@ -94,3 +94,36 @@ def test_tile_rows_cover_the_image_once():
         for h, rows in ((1080, 8), (512, 8), (17, 3), (5, 8)):
             got = sorted(y for r in range(world) for y in D.tile_rows(h, world, r, rows))
             assert got == list(range(h))
+
+
+def _tile_sort_worker(rank, world, port, out_path, scene, image, rows, sort):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = O.OracleScene(os.path.join(O.ASSETS, scene + ".scene"), image=image)
+    fb, st = sc.render_tiled(D.bucket_exchange(dist, torch), world, rank, tile_rows=rows, sort=sort, threads=2)
+    t = torch.from_numpy(fb)
+    dist.reduce(t, dst=0)                   # owners' pixels are disjoint, the rest 0: x + 0 = x exactly
+    live = torch.tensor([st["live_segments"]], dtype=torch.int64)
+    dist.reduce(live, dst=0)
+    if rank == 0:
+        np.save(out_path, t.numpy())
+        np.save(out_path + ".live.npy", live.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,scene,image,rows,sort", [
+    (2, "cornell_plus", (24, 16, 45, 5), 3, True),    # 3 passes, short last pass, 3-row stripes
+    (3, "teapot", (40, 22, 20, 8), 8, True),          # BVH + env map; 22 rows: a short last stripe
+    (2, "spheres", (20, 12, 20, 6), 4, True),
+    (2, "cornell", (24, 16, 20, 4), 5, False)])       # sort off: no exchange, slot = ray index
+def test_tile_sharded_sort_on_is_bitexact(tmp_path, world, scene, image, rows, sort):
+    """Pixel tiles WITH the reorder on: each owner renders only its stripes; after
+    every bounce but the last the owners all-reduce one byte per live ray (bucket + 1 at its global
+    slot) over gloo and rank their own rays by the global stable order, so every process seed is
+    the one the single-GPU render uses (raytracing.cu:89 after :238-247).  The assembled frame and
+    the live segment count equal the single-process oracle render bit for bit."""
+    out = str(tmp_path / "fb.npy")
+    mp.spawn(_tile_sort_worker, args=(world, _free_port(), out, scene, image, rows, sort), nprocs=world, join=True)
+    ref, rst = O.OracleScene(os.path.join(O.ASSETS, scene + ".scene"), image=image).render(sort=sort)
+    assert np.array_equal(np.load(out), ref)
+    assert int(np.load(out + ".live.npy")[0]) == rst["live_segments"]

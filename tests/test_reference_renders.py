@@ -24,6 +24,7 @@ import rtamd as R
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 STATS = json.load(open(os.path.join(HERE, "golden", "reference_render_stats.json")))["scenes"]
+SYSTEMATIC = 0.05   # 8-bit levels: the fast-math / tone-map rounding floor of a block-mean difference
 
 
 @pytest.mark.parametrize("scene", ["cornell", "cornell_plus", "spheres"])
@@ -49,9 +50,16 @@ def test_matches_reference_render_statistics(scene):
     # noise variance from adjacent-pixel pairs (tests/golden/make_reference_stats.py)
     v_ref = np.array(ref["thumb20_noise_var"])
     v_our = block_noise_var(img)
-    z = (thumb - np.array(ref["thumb20"])) / np.sqrt((v_ref + v_our) / 2500.0 + 1e-12)
+    # + a systematic floor of 0.05 levels: in near-noiseless blocks (spheres' sky: per-pixel variance
+    # 0.3) the estimates differ by ~0.1 level, the size of one-LSB tone-map rounding flips between
+    # nvcc --use_fast_math and IEEE arithmetic on a fraction of the pixels
+    z = (thumb - np.array(ref["thumb20"])) / np.sqrt((v_ref + v_our) / 2500.0 + SYSTEMATIC ** 2)
     print(scene, "block z: rms %.2f max %.2f, |z|>3: %d of %d" % (np.sqrt((z ** 2).mean()), np.abs(z).max(),
                                                                 (np.abs(z) > 3).sum(), z.size))
+    for k in np.argsort(-np.abs(z).reshape(-1))[:6]:
+        by, bx, ch = np.unravel_index(k, z.shape)
+        print("  block (%2d,%2d) ch %d: ours %.2f ref %.2f z %.2f (v %.1f / %.1f)" % (
+            by, bx, ch, thumb[by, bx, ch], ref["thumb20"][by][bx][ch], z[by, bx, ch], v_our[by, bx, ch], v_ref[by, bx, ch]))
     assert np.sqrt((z ** 2).mean()) < 1.6
     assert np.abs(z).max() < 6.0
     assert (np.abs(z) > 3).sum() <= 0.02 * z.size
