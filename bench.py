@@ -206,9 +206,6 @@ def main():
     if args.no_sort:
         sort = False
     tiles = args.shard == "tiles" or args.tile_share > 1
-    if tiles and sort:
-        ap.error("--shard tiles needs --no-sort: with the reorder on, process seeds follow the global "
-                 "post-sort slot (raytracing.cu:89), which a pixel tile cannot know")
     import make_envmap
     make_envmap.ensure_envmap(os.path.join(REPO, "assets", "teapot", "textures", "envmap.pfm"))
     t_load = time.perf_counter()
@@ -217,6 +214,24 @@ def main():
     P = scene.passes
     tile_split = (args.tile_share, 0) if args.tile_share > 1 else (world, rank)
     ren = rtamd.Renderer(scene, sort=sort, device=local, tiles=tile_split + (TILE_ROWS,) if tiles else None)
+    exchange = {"calls": 0, "bytes": 0, "s": 0.0}
+    if tiles and sort and tile_split[0] > 1:
+        # pixel tiles with the reorder on: one byte per global live ray per bounce,
+        # summed over the owners (torch.distributed all_reduce; RCCL's ncclAllReduce in the library's
+        # own multi-GPU path).  The 1-GPU --tile-share probe has no other owners: their slots are
+        # filled as terminated rays, so rank 0's own rays keep a complete (if smaller) global order.
+        def exchange_fn(arr):
+            t0 = time.perf_counter()
+            if use_dist and world > 1:
+                t = torch.from_numpy(arr).to("cuda")
+                dist.all_reduce(t)
+                arr[:] = t.cpu().numpy()
+            else:
+                arr[arr == 0] = 65
+            exchange["calls"] += 1
+            exchange["bytes"] += int(arr.size)
+            exchange["s"] += time.perf_counter() - t0
+        ren.set_exchange(exchange_fn)
 
     px3 = W * H * 3
     frame = None
@@ -418,7 +433,13 @@ def main():
                 "scene_load_s": round(load_s, 3),
                 "bvh_ms": round(scene.bvh_ms, 1),
                 **({"tile_share_probe": "rank 0's %d-row stripes of a %d-GPU split, on one GPU"
-                    % (TILE_ROWS, args.tile_share)} if args.tile_share > 1 else {}),
+                    % (TILE_ROWS, args.tile_share) + (" (sort on: the other owners' bucket bytes are filled as "
+                                                      "terminated rays)" if sort else "")} if args.tile_share > 1 else {}),
+                **({"tile_exchange": {"calls": exchange["calls"], "bytes": exchange["bytes"],
+                                      "host_s": round(exchange["s"], 4),
+                                      "def": "per-bounce bucket-byte exchanges of every run of this process (timed, "
+                                             "event, counter and frame legs), host time inside the exchange"}}
+                   if exchange["calls"] else {}),
             },
             "parity": parity,
             "roofline": roof,

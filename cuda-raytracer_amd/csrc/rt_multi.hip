@@ -22,6 +22,11 @@
 // job, ~280 MB per device, 1/7 of it per link), plus the gather's W*H*3*4 * (N-1)/N into device 0.
 // One host thread per device (RCCL's one-thread-per-device model for a single-process
 // communicator); device_count = 1 runs the same code with every exchange local.
+//
+// rt_opts.shard_tiles = 1 deals pixel tiles instead (§8e's natural shard): device k renders owner
+// k's row stripes of every pass; with sort on the owners all-reduce one byte per global live ray
+// after every bounce but the last (nccl_exchange), and the frame is an ncclReduce of the owners'
+// framebuffers.
 #include "rt_abi.h"
 
 #include <hip/hip_runtime.h>
@@ -177,6 +182,65 @@ int run_device(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int 
     return RT_OK;
 }
 
+// Pixel tiles with the reorder on: the per-bounce bucket bytes summed over the devices in place
+// (ncclAllReduce, uint8: every global slot has one owner, no byte exceeds 65), on the pass's stream.
+int nccl_exchange(void *user, uint8_t *bytes, uint64_t n, void *stream) {
+    const ncclResult_t r = ncclAllReduce(bytes, bytes, n, ncclUint8, ncclSum, *static_cast<ncclComm_t *>(user),
+                                         static_cast<hipStream_t>(stream));
+    return r == ncclSuccess ? 0 : -(int)r - 1;
+}
+
+// Device `st.rank`'s tiles: owner rank's tile_rows-row stripes of every pass, then an
+// ncclReduce of the owners' framebuffers to the root: every pixel has one owner and is 0 elsewhere,
+// so the sum is that owner's value bit for bit (x + 0 = x).
+int run_device_tiles(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int world, DevState &st,
+                     float *fb_out) {
+    MHIP(hipSetDevice(st.device));
+    const size_t px3 = (size_t)scene->width * scene->height * 3;
+    rt_opts o = *base;
+    o.device = st.device;
+    o.device_count = 0;
+    o.device_ids = nullptr;
+    o.shard_tiles = 0;
+    o.pass_begin = 0;
+    o.pass_count = -1;
+    o.pass_stride = 1;
+    o.tile_count = world;
+    o.tile_index = st.rank;
+    rt_renderer *ren = nullptr;
+    int rc = rt_renderer_create(scene, &o, &ren);
+    if (rc) return rc;
+    struct Guard {
+        rt_renderer *r;
+        float *d = nullptr;
+        hipStream_t s = nullptr;
+        ~Guard() {
+            if (d) (void)hipFree(d);
+            if (s) (void)hipStreamDestroy(s);
+            rt_renderer_destroy(r);
+        }
+    } g{ren};
+    if (o.sort && world > 1) {
+        rc = rt_renderer_set_exchange(ren, nccl_exchange, &comm, 1);
+        if (rc) return rc;
+    }
+    rt_stats s{};
+    using clk = std::chrono::high_resolution_clock;
+    rc = rtamd_renderer_run_pitched(ren, 0, -1, 1, nullptr, 0, &s);
+    if (rc) return rc;
+    st.stats = s;
+    MHIP(hipMalloc(reinterpret_cast<void **>(&g.d), px3 * sizeof(float)));
+    MHIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
+    rc = rt_renderer_copy_framebuffer(ren, g.d);
+    if (rc) return rc;
+    const auto t0 = clk::now();
+    MNCCL(ncclReduce(g.d, g.d, px3, ncclFloat32, ncclSum, 0, comm, g.s));
+    if (st.rank == 0) MHIP(hipMemcpyAsync(fb_out, g.d, px3 * sizeof(float), hipMemcpyDeviceToHost, g.s));
+    MHIP(hipStreamSynchronize(g.s));
+    st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    return RT_OK;
+}
+
 }  // namespace
 
 int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stats *stats) {
@@ -192,7 +256,8 @@ int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out
         for (int j = 0; j < k; j++)
             if (devs[j] == devs[k]) return rtamd::fail(RT_E_INVALID, "device_ids: a device is listed twice");
     }
-    if (opts->tile_count > 1) return rtamd::fail(RT_E_INVALID, "device_count and tile_count are exclusive");
+    if (opts->tile_count > 1) return rtamd::fail(RT_E_INVALID, "device_count and tile_count are exclusive "
+                                                              "(shard_tiles = 1 deals the tiles over the devices)");
     if (opts->pass_begin != 0 || (opts->pass_count != -1 && opts->pass_count != (scene->ray_count + 19) / 20) ||
         opts->pass_stride > 1)
         return rtamd::fail(RT_E_INVALID, "multi-device rt_render renders the whole frame (pass_begin 0, all passes)");
@@ -204,7 +269,8 @@ int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out
         st[k].device = devs[k];
         st[k].rank = k;
         th.emplace_back([&, k]() {
-            st[k].rc = run_device(scene, opts, comms[k], world, st[k], fb_out);
+            st[k].rc = opts->shard_tiles ? run_device_tiles(scene, opts, comms[k], world, st[k], fb_out)
+                                         : run_device(scene, opts, comms[k], world, st[k], fb_out);
             if (st[k].rc) st[k].err = rt_last_error();
         });
     }

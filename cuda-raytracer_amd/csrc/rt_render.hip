@@ -502,12 +502,14 @@ template <bool SORTED, int FIRST, bool INLINE = false>
 __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &pa, int slot,
                                             const float4 *__restrict__ geo, const float4 *__restrict__ tc,
                                             const uint32_t *__restrict__ rid, const float2 *__restrict__ hits,
-                                            uint32_t seed_term) {
+                                            uint32_t seed_term, const uint32_t *__restrict__ seed_of = nullptr) {
     // The seed follows the reference's slot (raytracing.cu:89): the position with sort on;
     // with sort off a ray keeps its original slot, which is its ray id.  At bounce 0 the
     // reference slot is the ray id (pixel-tile renders: mapped from this tile's slot).
     const uint32_t ray0 = first_ray<FIRST>(pa.map, (uint32_t)slot);   // bounce 0 only
-    const uint32_t seed_slot = (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
+    // Pixel tiles with the reorder on: the global post-sort slot, carried per ray (seed_of).
+    const uint32_t seed_slot = (!FIRST && seed_of) ? seed_of[slot]
+                               : (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
     Rng rng = pcg_seed(seed_slot * 4137874753u + seed_term);
     float closest;
     int index;
@@ -575,13 +577,14 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
                                                        float4 *__restrict__ acc, uint8_t *__restrict__ bkt,
                                                        const uint32_t *__restrict__ live_count,
                                                        const float2 *__restrict__ hits, uint32_t seed_term, int last,
-                                                       Counters *__restrict__ ctr) {
+                                                       Counters *__restrict__ ctr,
+                                                       const uint32_t *__restrict__ seed_of = nullptr) {
     const int L = (int)__builtin_amdgcn_readfirstlane(*live_count);
     unsigned hit = 0, miss = 0, hit_sphere = 0;
     for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
         const int slot = base + threadIdx.x;
         if (slot >= L) continue;
-        const Shaded sh = shade_one<SORTED, FIRST, INLINE>(S, pa, slot, geo, tc, rid, hits, seed_term);
+        const Shaded sh = shade_one<SORTED, FIRST, INLINE>(S, pa, slot, geo, tc, rid, hits, seed_term, seed_of);
         const V3 no = sh.no, nd = sh.nd, T = sh.T, C = sh.C;
         miss += sh.kind == 0;
         hit += sh.kind != 0;
@@ -720,7 +723,12 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
                                                               const uint32_t *__restrict__ offsets,
                                                               const uint32_t *__restrict__ totals,
                                                               float4 *__restrict__ geo_out, float4 *__restrict__ tc_out,
-                                                              uint32_t *__restrict__ rid_out, SlotMap map) {
+                                                              uint32_t *__restrict__ rid_out, SlotMap map,
+                                                              const uint32_t *__restrict__ gslot_in = nullptr,
+                                                              const uint32_t *__restrict__ newpos = nullptr,
+                                                              uint32_t *__restrict__ gslot_out = nullptr) {
+    // gslot_out (pixel tiles with the reorder on): each moved ray also carries its new global slot,
+    // newpos[its old global slot] (old global slot at bounce 0: the ray index, map.ray(item))
     const int n = (int)*live_count;
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
@@ -749,6 +757,8 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
             t = tc_in[item];
             id = FIRST_SRC ? first_ray<FIRST_SRC>(map, (uint32_t)item) : rid_in[item];
         }
+        uint32_t gs = 0;
+        if (gslot_out && move) gs = newpos[FIRST_SRC ? first_ray<FIRST_SRC>(map, (uint32_t)item) : gslot_in[item]];
         const unsigned long long peers = match_bucket(b, valid);
         const uint32_t rank = rank_below(peers);
         if (valid && rank == 0) wcount[wave][b] = (uint32_t)__popcll(peers);
@@ -760,6 +770,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
             geo_out[(size_t)pos * 2 + 1] = g1;
             tc_out[pos] = t;
             rid_out[pos] = id;
+            if (gslot_out) gslot_out[pos] = gs;
         }
         __syncthreads();
         if (threadIdx.x < kBuckets) {
@@ -770,6 +781,85 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
         __syncthreads();
     }
     }
+}
+
+// ---- pixel tiles with the reorder on: the global bucket array and the global rank
+// Every live ray of this owner writes bucket + 1 at its global slot (bounce 0: its ray index) of
+// the zeroed array G; the exchange sums G over the owners.
+__global__ __launch_bounds__(kBlock) void zero_bytes_kernel(uint8_t *__restrict__ g, const uint32_t *__restrict__ count) {
+    const uint32_t n = *count;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) g[i] = 0;
+}
+template <int FIRST>
+__global__ __launch_bounds__(kBlock) void tile_bytes_kernel(const uint8_t *__restrict__ bkt, const uint32_t *__restrict__ live_count,
+                                                            const uint32_t *__restrict__ gslot, SlotMap map,
+                                                            uint8_t *__restrict__ g) {
+    const uint32_t n = *live_count;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+        g[FIRST ? map.ray(i) : gslot[i]] = (uint8_t)(bkt[i] + 1);
+}
+// After the exchange: G holds bucket + 1 for every global live slot; back to buckets in place.  A
+// byte outside [1, 65] (a slot no owner wrote, or an exchange that did not sum) is counted in
+// *bad and made a terminated ray, so no bucket index ever leaves [0, 64]; the host fails the render.
+__global__ __launch_bounds__(kBlock) void unbias_bytes_kernel(uint8_t *__restrict__ g, const uint32_t *__restrict__ count,
+                                                              uint32_t *__restrict__ bad) {
+    const uint32_t n = *count;
+    uint32_t nbad = 0;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const uint32_t v = g[i];
+        const bool ok = v >= 1 && v <= kBuckets;
+        nbad += ok ? 0u : 1u;
+        g[i] = (uint8_t)(ok ? v - 1 : kDead);
+    }
+    if (nbad) atomicAdd(bad, nbad);
+}
+// The stable sort's new position of every live global slot (the scatter's ranking without the
+// move): newpos[g] = slots of smaller buckets + earlier slots of the same bucket.
+__global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__restrict__ bkt_in,
+                                                           const uint32_t *__restrict__ live_count, int tiles,
+                                                           const uint32_t *__restrict__ offsets,
+                                                           const uint32_t *__restrict__ totals,
+                                                           uint32_t *__restrict__ newpos) {
+    const int n = (int)*live_count;
+    __shared__ uint32_t run[kBuckets];
+    __shared__ uint32_t wcount[kBlock / 64][kBuckets];
+    for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int b = 0; b < kBuckets; b++) {
+                run[b] = acc + offsets[(size_t)b * tiles + tile];
+                acc += totals[b];
+            }
+        }
+        for (int k = threadIdx.x; k < (kBlock / 64) * kBuckets; k += kBlock) (&wcount[0][0])[k] = 0;
+        __syncthreads();
+        const int wave = threadIdx.x >> 6;
+        const int base = tile * kSortTile;
+        for (int r = 0; r < kSortItems; r++) {
+            const int item = base + r * kBlock + threadIdx.x;
+            const bool valid = item < n;
+            const uint32_t b = valid ? bkt_in[item] : 0u;
+            const unsigned long long peers = match_bucket(b, valid);
+            const uint32_t rank = rank_below(peers);
+            if (valid && rank == 0) wcount[wave][b] = (uint32_t)__popcll(peers);
+            __syncthreads();
+            if (valid && b != kDead) {
+                uint32_t pos = run[b] + rank;
+                for (int k = 0; k < wave; k++) pos += wcount[k][b];
+                newpos[item] = pos;
+            }
+            __syncthreads();
+            if (threadIdx.x < kBuckets) {
+                uint32_t s2 = 0;
+                for (int k = 0; k < kBlock / 64; k++) { s2 += wcount[k][threadIdx.x]; wcount[k][threadIdx.x] = 0; }
+                run[threadIdx.x] += s2;
+            }
+            __syncthreads();
+        }
+    }
+}
+__global__ void set_count_kernel(uint32_t *__restrict__ dst, uint32_t v, const uint32_t *__restrict__ src) {
+    if (threadIdx.x == 0) *dst = src ? *src : v;
 }
 
 // Fused reorder (shade_kernel<..., FUSED>): the shade kernel has written only the buckets (and the radiance of
@@ -979,12 +1069,21 @@ struct PassCtx {
     DevBuf<uint8_t> bkt;
     DevBuf<float2> hits;
     DevBuf<float> psum;               // this pass's per-pixel sums (when the caller gives no buffer)
+    // pixel tiles with the reorder on: global slot per ray (ping-pong with the state), the global
+    // bucket bytes, their ranks, the global live count {current, next} and its host copy
+    DevBuf<uint32_t> gslot[2], newpos, glive;
+    DevBuf<uint8_t> gbytes;
+    uint32_t *lg_host = nullptr;      // pinned
+    // state of this context's pass in the tiled sort-on schedule
+    int t_p = 0, t_rtc = 0, t_rem = 0, t_n = 0, t_cur = 0, t_tiles_g = 0;
+    uint64_t t_lg = 0;
     hipEvent_t fb_done = nullptr;     // recorded after this context last added into the framebuffer
     hipEvent_t done = nullptr;
     std::vector<hipEvent_t> events;   // (begin, end) pairs: process launches, then reorder launches
     size_t ev = 0;
 
     ~PassCtx() {
+        if (lg_host) (void)hipHostFree(lg_host);
         for (auto e : events) (void)hipEventDestroy(e);
         if (fb_done) (void)hipEventDestroy(fb_done);
         if (done) (void)hipEventDestroy(done);
@@ -1043,11 +1142,18 @@ struct rt_renderer {
     hipEvent_t t_begin = nullptr, t_end = nullptr;
 
     ~rt_renderer() {
+        if (xhost) (void)hipHostFree(xhost);
         if (t_begin) (void)hipEventDestroy(t_begin);
         if (t_end) (void)hipEventDestroy(t_end);
     }
 
     hipStream_t stream() const { return ctx[0].stream; }
+    // pixel tiles with the reorder on: the per-bounce bucket exchange (rt_renderer_set_exchange)
+    rt_exchange_fn xfn = nullptr;
+    void *xuser = nullptr;
+    bool x_on_device = false;
+    uint8_t *xhost = nullptr;         // pinned staging of a host exchange
+    bool tsort() const { return tile_count > 1 && sort; }
     int pass_count() const { return (spp + 19) / 20; }
     bool tiled() const { return tile_count > 1; }
     // Pixels of this owner's stripes (the last stripe of the image may be short).
@@ -1078,9 +1184,11 @@ struct rt_renderer {
         if (const char *f = std::getenv("RTAMD_INLINE")) inline_hits = fused && std::atoi(f) != 0 && sc->triangle_count == 0;
         if (tile_index < 0 || tile_index >= tile_count)
             return rtamd::fail(RT_E_INVALID, "tile_index outside [0, tile_count)");
-        if (tile_count > 1 && sort)
-            return rtamd::fail(RT_E_INVALID, "pixel-tile sharding needs sort off: with the reorder on, process seeds "
-                                             "follow the global post-sort slot (raytracing.cu:89)");
+        if (tsort()) {                  // per-bounce exchange between the kernels: the plain
+            fused = false;              // shade/scatter pair only
+            fused_upto = -1;
+            inline_hits = false;
+        }
         width = sc->width;
         height = sc->height;
         spp = sc->ray_count;
@@ -1210,6 +1318,14 @@ struct rt_renderer {
             if ((rc = c.hits.alloc((size_t)max_rays))) return rc;
             if ((rc = c.overflow.alloc((size_t)trace_blocks_max * kBlock * 2 * (kStackMax - kStackLds)))) return rc;
             if ((rc = c.psum.alloc((size_t)pixels * 3))) return rc;
+            if (tsort()) {
+                for (int q = 0; q < 2; q++)
+                    if ((rc = c.gslot[q].alloc((size_t)max_rays))) return rc;
+                if ((rc = c.newpos.alloc((size_t)max_rays)) || (rc = c.gbytes.alloc((size_t)max_rays)) ||
+                    (rc = c.glive.alloc(3)))
+                    return rc;
+                HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c.lg_host), sizeof(uint32_t)));
+            }
         }
         tm.mark("pass contexts");
         HIPCHK(hipMemsetAsync(fb.p, 0, fb.n * sizeof(float), s0));
@@ -1381,6 +1497,143 @@ struct rt_renderer {
         return RT_OK;
     }
 
+    // ---- pixel tiles with the reorder on (rt_renderer_set_exchange)
+    // A group of passes in flight advances bounce by bounce in lockstep: every pass's trace and shade
+    // (+ its bucket bytes) are enqueued, then pass by pass the bytes are exchanged (one host sync per
+    // pass and bounce: the all-reduce count is the global live count) and the global ranking and the
+    // local reorder are enqueued.  Every owner issues its exchanges in the same order.
+    int tsort_begin(PassCtx &c, int p) {
+        const int before = spp - 20 * p;
+        c.t_p = p;
+        c.t_rtc = std::min(before, 20);
+        c.t_rem = before - c.t_rtc;
+        c.t_n = (int)(c.t_rtc * tile_pixels());
+        c.t_cur = 0;
+        c.t_lg = (uint64_t)c.t_rtc * width * height;   // every generated ray is live at bounce 0
+        c.t_tiles_g = (int)((c.t_lg + kSortTile - 1) / kSortTile);
+        hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, c.stream, c.live.p, (uint32_t)c.t_n, bounces + 1,
+                           c.queue.p, nullptr);
+        hipLaunchKernelGGL(set_count_kernel, dim3(1), dim3(64), 0, c.stream, c.glive.p, (uint32_t)c.t_lg, nullptr);
+        HIPCHK(hipMemsetAsync(c.glive.p + 2, 0, sizeof(uint32_t), c.stream));
+        HIPCHK(hipGetLastError());
+        return RT_OK;
+    }
+    PassArgs tsort_args(const PassCtx &c) const {
+        const uint32_t stripe_px = (uint32_t)(tile_rows * width);
+        return PassArgs{c.t_rtc, 709579u * (uint32_t)c.t_rem, FastDiv::of((uint32_t)c.t_rtc), FastDiv::of((uint32_t)width),
+                        SlotMap::of(stripe_px * (uint32_t)c.t_rtc, tile_count, tile_index)};
+    }
+    // trace + shade of bounce b, then (but after the last bounce) this owner's bucket bytes
+    int tsort_front(PassCtx &c, int b, int64_t &sorted) {
+        hipStream_t st = c.stream;
+        const PassArgs pa = tsort_args(c);
+        const int grid = blocks_for(c.t_n);
+        const int tgrid = std::max(1, std::min(grid, trace_blocks));
+        const int sgrid = std::max(1, std::min(grid, cus * RT_SHADE_BPC));
+        const uint32_t seed_term = 279220567u * (uint32_t)(c.t_rem * 20 + b);
+        const uint32_t *lv = c.live.p + b;
+        uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
+        const int last = b + 1 == bounces;
+        const int cur = c.t_cur;
+        if (c.t_n == 0) return RT_OK;
+#define RT_TS(COUNT)                                                                                               \
+    do {                                                                                                           \
+        if (b == 0) {                                                                                              \
+            hipLaunchKernelGGL((trace_kernel<true, COUNT, 2>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
+            hipLaunchKernelGGL((shade_kernel<true, COUNT, 2, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
+                               pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
+                               seed_term, last, ctr.p, nullptr);                                                   \
+        } else {                                                                                                   \
+            hipLaunchKernelGGL((trace_kernel<true, COUNT, 0>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
+            hipLaunchKernelGGL((shade_kernel<true, COUNT, 0, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
+                               pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
+                               seed_term, last, ctr.p, c.gslot[cur].p);                                            \
+        }                                                                                                          \
+    } while (0)
+        if (counters) RT_TS(true); else RT_TS(false);
+#undef RT_TS
+        if (!last) {
+            const int zgrid = std::max(1, std::min(blocks_for((int64_t)c.t_lg), cus * 8));
+            hipLaunchKernelGGL(zero_bytes_kernel, dim3(zgrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p);
+            if (b == 0)
+                hipLaunchKernelGGL(tile_bytes_kernel<1>, dim3(sgrid), dim3(kBlock), 0, st, c.bkt.p, lv, c.gslot[cur].p,
+                                   pa.map, c.gbytes.p);
+            else
+                hipLaunchKernelGGL(tile_bytes_kernel<0>, dim3(sgrid), dim3(kBlock), 0, st, c.bkt.p, lv, c.gslot[cur].p,
+                                   pa.map, c.gbytes.p);
+            sorted += c.t_n;
+        }
+        HIPCHK(hipGetLastError());
+        return RT_OK;
+    }
+    // the exchange of bounce b's bytes, then the global ranking and this owner's reorder
+    int tsort_back(PassCtx &c, int b) {
+        hipStream_t st = c.stream;
+        const PassArgs pa = tsort_args(c);
+        HIPCHK(hipStreamSynchronize(st));
+        if (b > 0) c.t_lg = *c.lg_host;             // global live count after bounce b - 1
+        const uint64_t lg = c.t_lg;
+        if (lg > 0) {
+            int rc;
+            if (x_on_device) {
+                rc = xfn(xuser, c.gbytes.p, lg, st);
+            } else {
+                HIPCHK(hipMemcpyAsync(xhost, c.gbytes.p, lg, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                rc = xfn(xuser, xhost, lg, st);
+                if (!rc) HIPCHK(hipMemcpyAsync(c.gbytes.p, xhost, lg, hipMemcpyHostToDevice, st));
+            }
+            if (rc) return rtamd::fail(RT_E_INVALID, "tile exchange callback failed (" + std::to_string(rc) + ")");
+        }
+        const int tg = c.t_tiles_g;
+        const int ggrid = std::max(1, std::min((int)((lg + kSortTile - 1) / kSortTile), cus * 8));
+        const int bgrid = std::max(1, std::min(blocks_for((int64_t)lg), cus * 8));
+        // global: buckets of every live slot -> new global slots (newpos) and the next live count
+        hipLaunchKernelGGL(unbias_bytes_kernel, dim3(bgrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p, c.glive.p + 2);
+        hipLaunchKernelGGL(sort_hist_kernel, dim3(ggrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p, tg, c.sort_counts.p);
+        hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, c.glive.p, tg,
+                           c.sort_offsets.p, c.sort_totals.p, c.glive.p + 1);
+        hipLaunchKernelGGL(sort_rank_kernel, dim3(ggrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p, tg,
+                           c.sort_offsets.p, c.sort_totals.p, c.newpos.p);
+        hipLaunchKernelGGL(set_count_kernel, dim3(1), dim3(64), 0, st, c.glive.p, 0u, c.glive.p + 1);
+        HIPCHK(hipMemcpyAsync(c.lg_host, c.glive.p + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        // local: this owner's rays in the same stable order (local order = ascending global slot),
+        // each carrying its new global slot
+        const uint32_t *lv = c.live.p + b;
+        const int tiles = (c.t_n + kSortTile - 1) / kSortTile;
+        const int sort_grid = std::max(1, std::min(tiles, RT_SORT_GRID > 0 ? RT_SORT_GRID : cus * 8));
+        const int cur = c.t_cur;
+        hipLaunchKernelGGL(sort_hist_kernel, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, lv, tiles, c.sort_counts.p);
+        hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, lv, tiles,
+                           c.sort_offsets.p, c.sort_totals.p, c.live.p + b + 1);
+        if (b == 0)
+            hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                               c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p,
+                               c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, c.gslot[cur].p, c.newpos.p, c.gslot[1 - cur].p);
+        else
+            hipLaunchKernelGGL(sort_scatter_kernel<0>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                               c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p,
+                               c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, c.gslot[cur].p, c.newpos.p, c.gslot[1 - cur].p);
+        HIPCHK(hipGetLastError());
+        c.t_cur = 1 - cur;
+        return RT_OK;
+    }
+    int tsort_end(PassCtx &c, float *sums) {
+        hipStream_t st = c.stream;
+        const int64_t pixels = (int64_t)width * height;
+        const int64_t tpix = tile_pixels();
+        HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
+        if (bounces > 0 && tpix > 0) {
+            const SlotMap pix = SlotMap::of((uint32_t)(tile_rows * width), tile_count, tile_index);
+            hipLaunchKernelGGL(accumulate_kernel<true>, dim3((unsigned)((tpix + kAccPixels - 1) / kAccPixels)),
+                               dim3(kBlock), 0, st, c.acc.p, c.t_rtc, (int)tpix, sums, pix);
+        }
+        HIPCHK(hipGetLastError());
+        return RT_OK;
+    }
+
     // Closest hit of n caller rays (o.xyz, d.xyz; d unit length like every ray of the render):
     // the sphere loop and BVH traversal of one bounce (scene.cu:338-372, :134-241) through the
     // same trace_kernel as the render, without shading.
@@ -1464,19 +1717,54 @@ struct rt_renderer {
         int64_t sorted = 0, generated = 0;
         const int64_t px3 = (int64_t)width * height * 3;
         hipEvent_t prev_fb = nullptr;
-        for (int k = 0; k < count; k++) {
-            PassCtx &c = ctx[k % inflight];
-            const int p = pass_begin + k * stride;
-            float *sums = pass_sums ? pass_sums + (size_t)k * (pitch ? pitch : (size_t)px3) : c.psum.p;
-            const int rc = enqueue_pass(c, p, sums, sorted,
-                                        pass_events ? tspans.p + (size_t)k * 2 * (bounces + 1) : nullptr);
-            if (rc) return rc;
+        auto add_pass = [&](PassCtx &c, int p, float *sums) -> int {
             if (prev_fb) HIPCHK(hipStreamWaitEvent(c.stream, prev_fb, 0));
             hipLaunchKernelGGL(add_kernel, dim3(blocks_for(px3)), dim3(kBlock), 0, c.stream, fb.p, sums, (int)px3);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c.fb_done, c.stream));
             prev_fb = c.fb_done;
             generated += (int64_t)std::min(spp - 20 * p, 20) * tile_pixels();
+            return RT_OK;
+        };
+        auto sums_of = [&](PassCtx &c, int k) {
+            return pass_sums ? pass_sums + (size_t)k * (pitch ? pitch : (size_t)px3) : c.psum.p;
+        };
+        if (tsort()) {
+            if (!xfn) return rtamd::fail(RT_E_INVALID, "pixel tiles with sort on need the per-bounce exchange "
+                                                       "(rt_renderer_set_exchange)");
+            for (int g0 = 0; g0 < count; g0 += inflight) {
+                const int gn = std::min(inflight, count - g0);
+                for (int j = 0; j < gn; j++)
+                    if (int rc = tsort_begin(ctx[j], pass_begin + (g0 + j) * stride)) return rc;
+                for (int b = 0; b < bounces; b++) {
+                    for (int j = 0; j < gn; j++)
+                        if (int rc = tsort_front(ctx[j], b, sorted)) return rc;
+                    if (b + 1 != bounces)
+                        for (int j = 0; j < gn; j++)
+                            if (int rc = tsort_back(ctx[j], b)) return rc;
+                }
+                for (int j = 0; j < gn; j++) {
+                    float *sums = sums_of(ctx[j], g0 + j);
+                    if (int rc = tsort_end(ctx[j], sums)) return rc;
+                    if (int rc = add_pass(ctx[j], ctx[j].t_p, sums)) return rc;
+                    uint32_t bad = 0;
+                    HIPCHK(hipMemcpyAsync(&bad, ctx[j].glive.p + 2, sizeof(bad), hipMemcpyDeviceToHost, ctx[j].stream));
+                    HIPCHK(hipStreamSynchronize(ctx[j].stream));
+                    if (bad)
+                        return rtamd::fail(RT_E_INVALID, "tile exchange: " + std::to_string(bad) +
+                                                         " global slots had no owner's byte (the exchange must sum every owner's array)");
+                }
+            }
+        } else {
+            for (int k = 0; k < count; k++) {
+                PassCtx &c = ctx[k % inflight];
+                const int p = pass_begin + k * stride;
+                float *sums = sums_of(c, k);
+                const int rc = enqueue_pass(c, p, sums, sorted,
+                                            pass_events ? tspans.p + (size_t)k * 2 * (bounces + 1) : nullptr);
+                if (rc) return rc;
+                if (int rc2 = add_pass(c, p, sums)) return rc2;
+            }
         }
         for (int k = 1; k < inflight; k++) {
             HIPCHK(hipEventRecord(ctx[k].done, ctx[k].stream));
@@ -1517,7 +1805,7 @@ struct rt_renderer {
             // (reorder begin, end) pairs between them, in enqueue order.
             double proc = 0, srt = 0, trc = 0;
             uint64_t trace_launches = 0;
-            for (int q = 0; pass_events && q < inflight; q++) {
+            for (int q = 0; pass_events && !tsort() && q < inflight; q++) {
                 const int passes_here = count > q ? (count - q + inflight - 1) / inflight : 0;
                 size_t e = 0;
                 for (int r = 0; r < passes_here; r++)
@@ -1534,7 +1822,7 @@ struct rt_renderer {
             }
             // trace launches: the device wall-clock span from the first wave's start to the last
             // wave's end (the stream's events would add the queueing before the first wave)
-            if (pass_events && !inline_hits && count > 0) {
+            if (pass_events && !inline_hits && !tsort() && count > 0) {
                 std::vector<unsigned long long> sp((size_t)count * 2 * (bounces + 1));
                 HIPCHK(hipMemcpy(sp.data(), tspans.p, sp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
                 for (int k = 0; k < count; k++)
@@ -1713,6 +2001,19 @@ int rt_renderer_clear(rt_renderer *r) {
 int rt_renderer_set_event_timing(rt_renderer *r, int32_t enable) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
     r->pass_events = enable != 0;
+    return RT_OK;
+}
+
+int rt_renderer_set_exchange(rt_renderer *r, rt_exchange_fn fn, void *user, int32_t on_device) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    r->xfn = fn;
+    r->xuser = user;
+    r->x_on_device = on_device != 0;
+    if (fn && !r->x_on_device && !r->xhost && r->tsort()) {
+        HIPCHK(hipSetDevice(r->device));
+        const size_t n = (size_t)r->width * r->height * std::min(20, std::max(1, r->spp));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&r->xhost), n));
+    }
     return RT_OK;
 }
 

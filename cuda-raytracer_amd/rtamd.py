@@ -58,7 +58,11 @@ class RtOpts(C.Structure):
     _fields_ = [("sort", I32), ("device", I32), ("pass_begin", I32), ("pass_count", I32),
                 ("pass_stride", I32), ("collect_counters", I32),
                 ("tile_count", I32), ("tile_index", I32), ("tile_rows", I32),
-                ("device_count", I32), ("device_ids", C.POINTER(I32))]
+                ("device_count", I32), ("device_ids", C.POINTER(I32)), ("shard_tiles", I32)]
+
+
+# rt_exchange_fn: (user, bytes, n, hip_stream) -> 0 (pixel tiles with sort on, rt_renderer_set_exchange)
+EXCHANGE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_uint64, C.c_void_p)
 
 
 class RtStats(C.Structure):
@@ -238,7 +242,7 @@ def tile_rows_of(height, tile_count, tile_index, tile_rows=8):
 
 
 def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=1, counters=False,
-           tiles=None, devices=None):
+           tiles=None, devices=None, shard_tiles=False):
     """rt_render: the drop-in for gpu_raytrace.  Returns (framebuffer W*H*3 float32, stats).
     devices = list of device ordinals: the in-library multi-GPU render (pass sharding + RCCL
     slice exchange and gather; rt_opts.device_count/device_ids), also at one device."""
@@ -250,6 +254,7 @@ def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=
         ids = (I32 * len(devices))(*[int(d) for d in devices])
         o.device_count = len(devices)
         o.device_ids = C.cast(ids, C.POINTER(I32))
+        o.shard_tiles = int(shard_tiles)
     _check(lib().rt_render(scene.ptr, C.byref(o), _ptr(fb), C.byref(st)))
     return fb, st.as_dict()
 
@@ -288,6 +293,20 @@ class Renderer:
         st = RtStats()
         _check(lib().rt_renderer_run_host(self.h, pass_begin, count, stride, _ptr(out), C.byref(st)))
         return out, st.as_dict()
+
+    def set_exchange(self, exchange):
+        """Pixel tiles with sort on: exchange(arr) must sum the uint8 numpy array over all tile
+        owners in place (rt_renderer_set_exchange with a host buffer)."""
+        def cb(user, p, n, stream):
+            try:
+                exchange(np.ctypeslib.as_array(p, shape=(int(n),)))
+                return 0
+            except Exception:           # reported by the renderer as a failed exchange
+                return -1
+        self._exchange = EXCHANGE(cb)  # kept alive as long as the renderer
+        f = lib().rt_renderer_set_exchange
+        f.argtypes = [P, EXCHANGE, P, I32]
+        _check(f(self.h, self._exchange, None, 0))
 
     def set_counters(self, on):
         _check(lib().rt_renderer_set_counters(self.h, int(on)))

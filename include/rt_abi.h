@@ -103,9 +103,9 @@ typedef struct {
     /* Pixel-tile sharding: the image is cut into stripes of tile_rows rows, dealt
      * round-robin to tile_count owners; this render casts only the rays of owner tile_index's
      * stripes, with their global ray indices (so seeds are the 1-GPU ones), and leaves the other
-     * pixels 0.  Exact only with sort = 0: with the reorder on, process seeds follow the global
-     * post-sort slot (raytracing.cu:89, :238-247), which a tile cannot know; sort = 1 with
-     * tile_count > 1 is RT_E_INVALID.  tile_count 0 or 1 = the whole image (default). */
+     * pixels 0.  With sort = 1 the process seeds follow the global post-sort slot
+     * (raytracing.cu:89, :238-247), which needs the per-bounce exchange of
+     * rt_renderer_set_exchange.  tile_count 0 or 1 = the whole image (default). */
     int32_t tile_count;
     int32_t tile_index;
     int32_t tile_rows;    /* stripe height in rows; 0 = 8 */
@@ -118,6 +118,11 @@ typedef struct {
      * single device `device`.  The reference ran one device (raytracing.cu:170-284). */
     int32_t device_count;
     const int32_t *device_ids;
+    /* With device_count >= 1: 0 = pass sharding (above, the default); 1 = pixel tiles: device k
+     * renders owner k's tile_rows-row stripes of every pass, with sort on through the
+     * per-bounce bucket-byte ncclAllReduce (rt_renderer_set_exchange), and an ncclReduce of the
+     * owners' framebuffers (disjoint pixels, the rest 0) to device_ids[0]. */
+    int32_t shard_tiles;
 } rt_opts;
 
 typedef struct {
@@ -178,6 +183,18 @@ int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out);   /* device fb 
 int rt_renderer_copy_framebuffer(rt_renderer *r, float *d_out);    /* device fb -> device ptr on
                                                                        r's device (W*H*3 floats) */
 int rt_renderer_clear(rt_renderer *r);                               /* zero the device fb    */
+/* Pixel tiles with the reorder on (tile_count > 1, sort = 1).  The process seed is the
+ * ray's GLOBAL post-sort slot (raytracing.cu:89 after :238-247), so after every bounce but the
+ * last the owners exchange one byte per global live ray: each writes bucket + 1 at the global slot
+ * of each of its live rays into a zeroed array of n bytes, and `exchange` must sum the arrays of
+ * all owners in place (an all-reduce: every slot has one owner, no byte exceeds 65) and return 0.
+ * Each owner then ranks its rays as the stable sort of all keys would; rays never migrate.
+ * on_device = 1: `bytes` is a device pointer on the renderer's device and the exchange is enqueued
+ * on (or completed before returning from) `hip_stream`, a hipStream_t; 0: `bytes` is host memory
+ * and the exchange completes before returning.  Calls come in the same order on every owner
+ * (pass by pass of a group in flight, bounce by bounce).  Without an exchange such a render fails. */
+typedef int (*rt_exchange_fn)(void *user, uint8_t *bytes, uint64_t n, void *hip_stream);
+int rt_renderer_set_exchange(rt_renderer *r, rt_exchange_fn fn, void *user, int32_t on_device);
 int rt_renderer_set_counters(rt_renderer *r, int32_t enable);
 /* Per-bounce HIP events behind rt_stats.process_ms / sort_ms (default on).  Off, those stay 0 and
  * a pass's stream carries no marker packets between its kernels (~2 % faster frames). */

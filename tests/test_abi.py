@@ -40,7 +40,7 @@ def test_library_is_gfx950_and_links_hip():
 def test_struct_layouts():
     # sizes fixed by the reference layouts (scene.cuh:9-100) and by rt_abi.h
     assert C.sizeof(R.RtScene) == 216
-    assert C.sizeof(R.RtOpts) == 48   # + tile_count, tile_index, tile_rows, device_count, device_ids*
+    assert C.sizeof(R.RtOpts) == 56   # + tile_count/index/rows, device_count, device_ids*, shard_tiles
     assert C.sizeof(R.RtLoadOpts) == 48
     assert C.sizeof(R.RtStats) == 11 * 8 + 8 + 5 * 8 + 8 + 8
     assert R.lib().rt_abi_version() == 3
@@ -51,7 +51,7 @@ def test_default_options():
     R.lib().rt_default_opts(C.byref(o))
     assert (o.sort, o.device, o.pass_begin, o.pass_count, o.pass_stride, o.collect_counters) == (1, 0, 0, -1, 1, 0)
     assert (o.tile_count, o.tile_index, o.tile_rows) == (0, 0, 0)   # whole image, 8-row stripes
-    assert o.device_count == 0 and not o.device_ids                  # one device, no RCCL
+    assert o.device_count == 0 and not o.device_ids and o.shard_tiles == 0   # one device, no RCCL
 
 
 def test_tile_rows_of():

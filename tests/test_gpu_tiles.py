@@ -1,8 +1,8 @@
 """Pixel-tile sharding (rt_opts.tile_*): a render restricted to one owner's row
 stripes, with sort off, equals the whole-image render on those rows bit for bit and leaves the
-other rows 0, so the owners' images add up to the 1-GPU image exactly.  With sort on a tile
-cannot know the global post-sort slots the process seeds follow (raytracing.cu:89), and the
-renderer refuses it."""
+other rows 0, so the owners' images add up to the 1-GPU image exactly.  With sort on the process
+seeds follow the global post-sort slots (raytracing.cu:89): the owners exchange one byte per
+global live ray per bounce (rt_renderer_set_exchange), and without an exchange the render fails."""
 import numpy as np
 import pytest
 
@@ -74,9 +74,60 @@ def test_tile_renderer_passes_in_flight(gpu):
     assert np.array_equal(fb.reshape(40, 64, 3)[rows], full.reshape(40, 64, 3)[rows])
 
 
-def test_tiles_with_sort_on_are_refused(gpu):
+def test_tiles_with_sort_on_need_an_exchange(gpu):
     psc = R.Scene("%s/cornell.scene" % R.ASSETS, image=(32, 32, 4, 2))
-    with pytest.raises(R.RtError, match="sort off"):
+    with pytest.raises(R.RtError, match="exchange"):
         R.render(psc, sort=True, tiles=(2, 0))
     with pytest.raises(R.RtError, match="tile_index"):
         R.render(psc, sort=False, tiles=(2, 2))
+
+
+@pytest.mark.parametrize("scene,image,rows,owners", [("cornell_plus", (48, 40, 45, 6), 8, 2),
+                                                     ("teapot", (64, 36, 20, 16), 4, 3),
+                                                     ("spheres", (40, 24, 20, 8), 8, 2)])
+def test_tiles_with_sort_on_bitexact(scene, image, rows, owners):
+    """Pixel tiles WITH the reorder on: `owners` renderers on this GPU, one per tile
+    owner, each in its own thread, exchange one byte per global live ray after every bounce but the
+    last (rt_renderer_set_exchange; here a host-side sum over the owners, RCCL's ncclAllReduce in
+    the multi-GPU library path) and rank their rays by the global stable order.  Their framebuffers
+    (disjoint pixels) add up to the oracle's single-process render bit for bit, and the live segment
+    counts add up to the oracle's."""
+    import threading
+    if R.device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on the MI355X box")
+    path = "%s/%s.scene" % (R.ASSETS, scene)
+    ref, rst = O.OracleScene(path, image=image).render(sort=True)
+    sc = R.Scene(path, image=image)
+    bar = threading.Barrier(owners, timeout=60)
+    parts, out, errs = {}, {}, []
+
+    def exchange_for(i):
+        def ex(arr):
+            parts[i] = arr.copy()
+            bar.wait()
+            tot = sum(parts[k].astype(np.int32) for k in range(owners))
+            bar.wait()
+            arr[:] = tot.astype(np.uint8)
+        return ex
+
+    def run(i):
+        try:
+            r = R.Renderer(sc, sort=True, tiles=(owners, i, rows))
+            r.set_exchange(exchange_for(i))
+            st = r.run(pass_begin=0, count=-1)
+            out[i] = (r.framebuffer(), st)
+            r.close()
+        except Exception as e:      # a failed owner would leave the others at the barrier
+            errs.append(e)
+            bar.abort()
+    th = [threading.Thread(target=run, args=(i,)) for i in range(owners)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    fb = np.zeros_like(ref)
+    for i in range(owners):
+        fb = fb + out[i][0]
+    assert np.array_equal(fb, ref)
+    assert sum(out[i][1]["live_segments"] for i in range(owners)) == rst["live_segments"]
