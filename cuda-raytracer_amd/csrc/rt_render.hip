@@ -23,7 +23,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
-#include <thread>
 #include <vector>
 
 #pragma clang fp contract(off)
@@ -243,6 +242,9 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 // do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
 // 8 waves per SIMD (<= 64 VGPRs): the one spill left is a lane constant reloaded only on the
 // overflow-stack path.  +2 % over the unconstrained 66 VGPRs (7 waves).
+#ifndef RT_PREFETCH
+#define RT_PREFETCH 0                 // 1: fetch an internal node's child-pair line during its slab tests; 2: + leaf
+#endif
 #ifndef RT_TRACE_WPE
 #define RT_TRACE_WPE 8
 #endif
@@ -381,6 +383,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         // node's interleaved child bounds and child refs), issued before the branch, so a step
         // costs one memory round trip whatever mix of leaf and internal lanes the wave holds.
         bool need = false;              // the lane needs the next node from its stack
+#if RT_PREFETCH
+        float pf = 0.0f;                // line fetched ahead for the next step (consumed at the step's end)
+#endif
         const bool in_leaf = ti < te;
         const float4 *rec = in_leaf ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4;
         const float4 a = rec[0], b = rec[1], c = rec[2];
@@ -397,6 +402,14 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             need = ++ti == te;
         } else {
             if (COUNT) iv++;
+#if RT_PREFETCH
+            // the children's records are siblings (one 128-B line): fetch the line while the slabs
+            // run, so the next step's record load finds it in L1/L2 when the lane descends
+            {
+                const uint32_t kin = (kids.x & kLeaf) ? kids.y : kids.x;
+                if (!(kin & kLeaf)) pf = S.nodes[(size_t)kin * 4].x;
+            }
+#endif
             float t0, t1;
             bool h0, h1;
             slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
@@ -436,6 +449,10 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 }
             }
         }
+#if RT_PREFETCH >= 2
+        // ... and the first triangle of a leaf the lane has just entered
+        if (ti < te && !in_leaf) pf += S.tris[(size_t)ti * 3].x;
+#endif
 #ifdef RT_PROFILE
         if (__ballot(need)) PROF(5, 1);
 #endif
@@ -466,6 +483,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 need = ti == te;
             }
         }
+#if RT_PREFETCH
+        asm volatile("" ::"v"(pf));     // keeps the fetch; its wait lands here, after the step's work
+#endif
     }
     Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
     const unsigned long long nl = wave_sum(nlive);
@@ -2041,19 +2061,10 @@ int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stat
     if (rc) return rc;
     const double t_create = ms_since(w0);
     auto w1 = clk::now();
-    // The caller's framebuffer is page-locked while the passes render (a pageable 12-MB D2H ran at
-    // ~1.2 GB/s: 10 ms of a 1000x1000 CLI render's span), so the read-back is a direct DMA.
-    bool pinned = false;
-    std::thread pin([&] {
-        pinned = hipHostRegister(fb_out, (size_t)scene->width * scene->height * 3 * sizeof(float),
-                                 hipHostRegisterDefault) == hipSuccess;
-    });
     rc = r->run(o.pass_begin, o.pass_count, o.pass_stride, nullptr, stats);
-    pin.join();
     const double t_run = ms_since(w1);
     w1 = clk::now();
     if (!rc) rc = rt_renderer_read_framebuffer(r, fb_out);
-    if (pinned) (void)hipHostUnregister(fb_out);
     const double t_read = ms_since(w1);
     w1 = clk::now();
     const int inflight = r->nctx;

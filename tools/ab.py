@@ -31,7 +31,7 @@ def main():
             for kv in filter(None, extra_env.split(",")):
                 k, _, v = kv.partition("=")
                 env[k] = v
-            out = subprocess.run([sys.executable, "bench.py", "--no-cpu-baseline", "--no-counters"] + extra,
+            out = subprocess.run([sys.executable, "bench.py", "--no-extras"] + extra,
                                  cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print("variant %s failed rc=%d: %s" % (n, out.returncode, out.stderr[-2000:]), flush=True)
