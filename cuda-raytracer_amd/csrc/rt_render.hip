@@ -1156,6 +1156,7 @@ struct rt_renderer {
     int wall_khz = 0;                    // device wall clock rate (wall_clock64 ticks per ms)
     PassCtx ctx[kInflight];
     int trace_blocks = 0;             // persistent trace_kernel grid of the current run
+    int trace_blocks_heavy = 0;       // ... for bounces 0 and 1
     int trace_blocks_max = 0;         // all resident trace workgroups (the overflow stacks are sized for it)
     int nctx = 1;                     // pass contexts allocated (passes in flight)
     int cus = 0;
@@ -1387,7 +1388,7 @@ struct rt_renderer {
         const int n = (int)(rtc * tpix);
         const int grid = blocks_for(n);
         const int tiles = (n + kSortTile - 1) / kSortTile;
-        const int tgrid = std::min(grid, trace_blocks);
+        int tgrid = std::min(grid, trace_blocks);
         const int sgrid = std::min(grid, cus * RT_SHADE_BPC);
         // tile-stride reorder kernels on at most 8 blocks per CU: in the tail bounces a block per
         // possible tile dispatched ~10^4 empty workgroups per launch (A/B: +0.3-0.5 %)
@@ -1422,6 +1423,7 @@ struct rt_renderer {
             const uint32_t *lv = c.live.p + b;
             uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
             const bool last = b + 1 == bounces;
+            tgrid = std::min(grid, b <= 1 ? trace_blocks_heavy : trace_blocks);
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
@@ -1724,6 +1726,11 @@ struct rt_renderer {
             const int pct = kTraceOccPct > 0 ? kTraceOccPct
                                              : std::min(100, std::max(RT_TRACE_OCC_MIN, 200 / concurrent));
             trace_blocks = std::max(1, trace_blocks_max * pct / 100);
+            // RTAMD_TRACE_HEAVY (A/B knob): % of the resident workgroups for the bounce-0/1 launches,
+            // which hold nearly every ray of a pass (0: the same grid as the tail bounces)
+            const char *h = std::getenv("RTAMD_TRACE_HEAVY");
+            const int hp = h ? std::atoi(h) : 0;
+            trace_blocks_heavy = hp > 0 ? std::max(1, trace_blocks_max * std::min(100, hp) / 100) : trace_blocks;
         }
         hipStream_t s0 = stream();
         if (pass_events && tspans.n < (size_t)std::max(count, 1) * 2 * (bounces + 1)) {

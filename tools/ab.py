@@ -31,14 +31,17 @@ def main():
             for kv in filter(None, extra_env.split(",")):
                 k, _, v = kv.partition("=")
                 env[k] = v
-            out = subprocess.run([sys.executable, "bench.py", "--no-extras"] + extra,
+            base_args = os.environ.get("AB_ARGS", "--no-extras").split()
+            out = subprocess.run([sys.executable, "bench.py"] + base_args + extra,
                                  cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print("variant %s failed rc=%d: %s" % (n, out.returncode, out.stderr[-2000:]), flush=True)
                 sys.exit(1)
             rec = json.loads(out.stdout.strip().splitlines()[-1])
             res[n].append((rec["ms_per_step"], rec["config"]["process_ms_per_step"], rec["value"]))
-            print("round %d %-12s ms/step %.3f process %.3f Mrays/s %.1f" % (r, n, *res[n][-1]), flush=True)
+            print("round %d %-12s ms/step %.3f process %.3f Mrays/s %.1f trace/step %s sort/step %s" % (
+                r, n, *res[n][-1], rec["config"].get("trace_ms_per_step"), rec["config"].get("sort_ms_per_step")),
+                flush=True)
     print("summary (median / min ms_per_step, median process ms, median Mrays/s):")
     for n in names:
         ms = [x[0] for x in res[n]]
