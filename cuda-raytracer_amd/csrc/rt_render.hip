@@ -1155,6 +1155,7 @@ struct rt_renderer {
     DevBuf<unsigned long long> tspans;   // per run: [pass][bounce] trace-launch wall-clock spans (event timing on)
     int wall_khz = 0;                    // device wall clock rate (wall_clock64 ticks per ms)
     PassCtx ctx[kInflight];
+    int pass_hint = 0;                // rt_render: the passes this renderer will ever run (0: any)
     int trace_blocks = 0;             // persistent trace_kernel grid of the current run
     int trace_blocks_heavy = 0;       // ... for bounces 0 and 1
     int trace_blocks_max = 0;         // all resident trace workgroups (the overflow stacks are sized for it)
@@ -1318,6 +1319,7 @@ struct rt_renderer {
         // 20 contexts ran a 13-pass share at 12.7 instead of 8.1 ms/pass)
         size_t cap = kInflight;
         if (const char *e = std::getenv("RTAMD_INFLIGHT")) cap = std::min<size_t>(cap, (size_t)std::max(1, std::atoi(e)));
+        if (pass_hint > 0) cap = std::min<size_t>(cap, (size_t)pass_hint);   // a one-shot render of fewer passes
         nctx = !passes ? 0 : (int)std::min<size_t>({cap, (size_t)std::max(1, pass_count()),
                                                     std::max<size_t>(1, mem_free / 2 / ctx_bytes)});
         const int inflight = nctx;
@@ -1798,7 +1800,11 @@ struct rt_renderer {
             HIPCHK(hipStreamWaitEvent(s0, ctx[k].done, 0));
         }
         HIPCHK(hipEventRecord(t_end, s0));
+        const double enq_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
         HIPCHK(hipStreamSynchronize(s0));
+        if (std::getenv("RTAMD_TIMING"))
+            std::fprintf(stderr, "rt_renderer run: %d passes enqueued in %.2f ms (host), done at %.2f ms\n", count, enq_ms,
+                         std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count());
 #ifdef RT_PROFILE
         {
             unsigned long long pr[2][12];
@@ -1958,7 +1964,8 @@ int rt_device_warmup(int32_t device) {
     return RT_OK;
 }
 
-int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer **out) {
+namespace {
+int create_renderer(const rt_scene *scene, const rt_opts *opts, rt_renderer **out, int pass_hint) {
     if (!out) return rtamd::fail(RT_E_INVALID, "null output");
     *out = nullptr;
     int rc = check_scene(scene);
@@ -1967,10 +1974,16 @@ int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer *
     if (opts) o = *opts; else rt_default_opts(&o);
     if (rt_device_count() <= o.device || o.device < 0) return rtamd::fail(RT_E_NODEVICE, "no such HIP device");
     auto *r = new rt_renderer();
+    r->pass_hint = pass_hint;
     rc = r->init(scene, &o);
     if (rc) { delete r; return rc; }
     *out = r;
     return RT_OK;
+}
+}  // namespace
+
+int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer **out) {
+    return create_renderer(scene, opts, out, 0);
 }
 
 int rtamd_renderer_run_pitched(rt_renderer *r, int pass_begin, int count, int stride, float *d_pass_sums,
@@ -2064,7 +2077,11 @@ int rt_render(const rt_scene *scene, const rt_opts *opts, float *fb_out, rt_stat
         return rc ? rc : rtamd_render_multi(scene, &o, fb_out, stats);
     }
     rt_renderer *r = nullptr;
-    int rc = rt_renderer_create(scene, &o, &r);
+    // contexts only for the passes this call renders (a one-pass render needs one, not 20)
+    const int P = (scene->ray_count + 19) / 20;
+    const int stride = std::max(1, o.pass_stride);
+    const int hint = o.pass_count >= 0 ? o.pass_count : std::max(0, (P - o.pass_begin + stride - 1) / stride);
+    int rc = create_renderer(scene, &o, &r, std::max(1, hint));
     if (rc) return rc;
     const double t_create = ms_since(w0);
     auto w1 = clk::now();
