@@ -340,10 +340,11 @@ def main():
         if full_frame:
             frame_s = elapsed
         else:
-            # the metric's render-wall column is a full frame: time one (untimed for `value`)
+            # the metric's render-wall column is a full frame: time one (untimed for `value`); with the
+            # weak-scaling extension, the configured frame's number of rounds of the extended one
             barrier_sync()
             f0 = time.perf_counter()
-            run_steps(R, {})
+            run_steps(R if frame_spp == spp else -(-(-(-spp // 20)) // world), {})
             barrier_sync()
             frame_s = time.perf_counter() - f0
         if not tiles and rank == 0:
@@ -435,8 +436,10 @@ def main():
                                 "pass-shard x%d + RCCL all-to-all/gather" % world) if world > 1 else "single GPU",
                 "nominal_mrays_per_s": round(nominal, 2),
                 "render_wall_def": "one full frame (%d passes), first pass to the accumulated framebuffer on the "
-                                   "GPU, inputs resident (%s)" % (P, "the timed region" if full_frame else
-                                                                  "an untimed full-frame leg after the timed steps"),
+                                   "GPU, inputs resident (%s)" % (-(-spp // 20), "the timed region" if full_frame else
+                                                                  "an untimed full-frame leg after the timed steps" +
+                                                                  ("; its rounds of full 20-spp passes of the extended "
+                                                                   "frame" if frame_spp != spp else "")),
                 "passes_per_frame": P,
                 **({"frame_extended": "%d spp (%d passes) instead of %d, so that each of the %d GPUs renders its %d "
                                       "passes in one batch" % (frame_spp, P, spp, world, steps)}
