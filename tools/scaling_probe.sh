@@ -9,10 +9,10 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 for n in 13 26 52; do
   # a rank's share through the torch.distributed (RCCL) path, as the driver's N>1 runs render it
-  timeout -k 10 300 python bench.py --steps $n --dist --no-counters --no-cpu-baseline "$@" > $OUT/steps$n.json 2> $OUT/steps$n.err || { tail $OUT/steps$n.err; exit 1; }
+  timeout -k 10 300 python bench.py --steps $n --dist --no-extras "$@" > $OUT/steps$n.json 2> $OUT/steps$n.err || { tail $OUT/steps$n.err; exit 1; }
   python3 -c "import json;d=json.load(open('$OUT/steps$n.json'));print($n,d['ms_per_step'],d['value'])"
 done
-timeout -k 10 300 python bench.py --no-counters --no-cpu-baseline "$@" > $OUT/full.json 2> $OUT/full.err || { tail $OUT/full.err; exit 1; }
+timeout -k 10 300 python bench.py --no-extras "$@" > $OUT/full.json 2> $OUT/full.err || { tail $OUT/full.err; exit 1; }
 python3 -c "import json;d=json.load(open('$OUT/full.json'));print('full',d['ms_per_step'],d['value'])"
-timeout -k 10 300 python bench.py --dist --no-counters --no-cpu-baseline "$@" > $OUT/dist.json 2> $OUT/dist.err || { tail $OUT/dist.err; exit 1; }
+timeout -k 10 300 python bench.py --dist --no-extras "$@" > $OUT/dist.json 2> $OUT/dist.err || { tail $OUT/dist.err; exit 1; }
 python3 -c "import json;d=json.load(open('$OUT/dist.json'));print('dist',d['ms_per_step'],d['value'])"
