@@ -39,8 +39,8 @@ if [ "$PART" = A ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-counters > $OUT/prof.log 2>&1 || { tail $OUT/prof.log; exit 1; }
   python3 tools/trace_summary.py trace $OUT/prof/run_kernel_trace.csv > $OUT/kernel_trace_summary_teapot.txt || exit 1
 else
-  for cfg in cornell_plus spheres lamp teapot_--no-sort lamp_--no-sort cornell; do
-    args=$(echo $cfg | tr '_' ' '); name=$(echo $cfg | tr -d '_-'); step bench $args
+  for cfg in cornell_plus spheres lamp teapot:--no-sort lamp:--no-sort cornell; do
+    args=$(echo $cfg | tr ':' ' '); name=$(echo $cfg | tr -d ':-'); step bench $args
     timeout -k 10 400 python bench.py --scene $args > $OUT/bench_$name.json 2> $OUT/bench_$name.err || { tail $OUT/bench_$name.err; exit 1; }
   done
   step strong-scaling probe
