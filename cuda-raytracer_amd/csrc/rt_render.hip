@@ -242,6 +242,9 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 // do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
 // 8 waves per SIMD (<= 64 VGPRs): the one spill left is a lane constant reloaded only on the
 // overflow-stack path.  +2 % over the unconstrained 66 VGPRs (7 waves).
+#ifndef RT_SEL
+#define RT_SEL 0                      // 1: next/near child chosen by one predicate (fewer selects)
+#endif
 #ifndef RT_PREFETCH
 #define RT_PREFETCH 0                 // 1: fetch an internal node's child-pair line during its slab tests; 2: + leaf
 #endif
@@ -286,6 +289,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     V3 o{0, 0, 0}, d{0, 0, 0};
     float ix = 0, iy = 0, iz = 0, closest = 0;
     bool finite_inv = true;
+#if RT_SEL
+    bool wave_nonfinite = false;        // some lane's ray has an infinite 1/d component (set at refill)
+#endif
     int index = -1, sp = 0;
     uint32_t ref = 0;
     int ti = 0, te = 0;                 // the lane is in a leaf while ti < te
@@ -337,6 +343,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     }
                     ix = 1 / d.x; iy = 1 / d.y; iz = 1 / d.z;
                     finite_inv = __builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz);
+
                     closest = 1e30f;
                     index = -1;
                     for (int i = 0; i < S.sphere_count; i++) {
@@ -357,6 +364,11 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     }
                 }
             }
+#if RT_SEL
+            // one ballot per refill instead of one per node step; the flag stays set until the next
+            // refill even if that ray has finished (the per-lane fold below is exact for every lane)
+            wave_nonfinite = __ballot(slot >= 0 && !finite_inv) != 0;
+#endif
         }
         if (!__ballot(slot >= 0)) {
             if (exhausted) break;
@@ -413,7 +425,11 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             float t0, t1;
             bool h0, h1;
             slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
+#if RT_SEL
+            if (__builtin_expect(wave_nonfinite, 0)) {
+#else
             if (__builtin_expect(__ballot(!finite_inv) != 0, 0)) {
+#endif
                 // some lane's 1/d has an infinite component (0 * inf may give NaN): the literal
                 // per-axis fold for those lanes
                 float u0, u1;
@@ -424,22 +440,35 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             // The reference pushes the hit children near then far (scene.cu:204-225) and pops the
             // top: with both hit the far child is next and the near one stays on the stack; with
             // one hit that one is next.  Next is entered unless its entry distance >= closest.
+#if RT_SEL
+            const bool both = h0 && h1, any = h0 || h1;
+            // next = child 1 iff it is the far child of two hits (t0 < t1; a tie makes child 1 the
+            // near one) or the only hit; the other child is the near one, pushed when both hit
+            const bool sel1 = h1 && (!h0 || t0 < t1);
+            const uint32_t next_ref = sel1 ? kids.y : kids.x, near_ref = sel1 ? kids.x : kids.y;
+            const float next_t = sel1 ? t1 : t0, near_t = sel1 ? t0 : t1;
+#else
             const bool both = h0 & h1, any = h0 | h1;
             const bool x_near = t0 < t1;
             const uint32_t near_ref = x_near ? kids.x : kids.y, far_ref = x_near ? kids.y : kids.x;
             const float near_t = x_near ? t0 : t1, far_t = x_near ? t1 : t0;
             const uint32_t next_ref = both ? far_ref : (h0 ? kids.x : kids.y);
             const float next_t = both ? far_t : (h0 ? t0 : t1);
+#endif
             // the near child is written either way (above the top when not pushed; entry
             // kStackLds is a scratch slot), so the push needs no branch
             col[min(sp, kStackLds) * kBlock] = make_uint2(near_ref, __float_as_uint(near_t));
-            if (__builtin_expect(both & (sp >= kStackLds), 0)) {
+            if (__builtin_expect(both && sp >= kStackLds, 0)) {
                 overflow[(sp - kStackLds) * lanes + gl] = near_ref;
                 overflow[dist_half + (sp - kStackLds) * lanes + gl] = __float_as_uint(near_t);
             }
+#if RT_SEL
+            if (both) sp++;
+#else
             sp += both ? 1 : 0;
+#endif
             ref = any ? next_ref : ref;
-            const bool descend = any & !(next_t >= closest);
+            const bool descend = any && !(next_t >= closest);
             need = !descend;
             if (descend) {
                 if (COUNT) pn++;
