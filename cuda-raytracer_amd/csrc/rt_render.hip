@@ -243,7 +243,10 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 // 8 waves per SIMD (<= 64 VGPRs): the one spill left is a lane constant reloaded only on the
 // overflow-stack path.  +2 % over the unconstrained 66 VGPRs (7 waves).
 #ifndef RT_SEL
-#define RT_SEL 0                      // 1: next/near child chosen by one predicate (fewer selects)
+// 1: next/near child chosen by one predicate, the non-finite-1/d check as one ballot per refill instead
+// of one per node step, logical (not bitwise) predicates.  A/B (4 rounds, teapot full frame): 7.50-7.65
+// -> 7.28-7.37 ms/pass; 20 steps 7.87 -> 7.67.  0 keeps the round-1 step for A/B.
+#define RT_SEL 1
 #endif
 #ifndef RT_PREFETCH
 #define RT_PREFETCH 0                 // 1: fetch an internal node's child-pair line during its slab tests; 2: + leaf
