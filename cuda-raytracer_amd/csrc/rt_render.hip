@@ -224,43 +224,6 @@ __device__ __forceinline__ void slab_pair(float4 a, float4 b, float4 c, V3 o, fl
     h1 = n1 <= f1;
 }
 
-// 1/a, bit-identical to the IEEE quotient the reference semantics ask for: v_rcp_f32 and one FMA
-// Newton step give the correctly rounded 1/a for every |a| in [2^-125, 2^125] on gfx950 (all 2^32
-// inputs checked, tools/experiments/rcp_check.hip); a wave with a lane outside that range (zero,
-// denormal, huge, inf, NaN) divides for those lanes.  3 VALU instead of the division's 10 on the
-// VALU-bound traversal step (RT_RCP=0 restores the division).
-#ifndef RT_RCP
-#define RT_RCP 1
-#endif
-__device__ __forceinline__ float recip(float a) {
-#if RT_RCP
-    const float r = __builtin_amdgcn_rcpf(a);
-    const float r1 = __builtin_fmaf(__builtin_fmaf(-a, r, 1.0f), r, r);
-    const float aa = __builtin_fabsf(a);
-    const bool ok = aa >= 0x1p-125f && aa <= 0x1p125f;
-    if (__builtin_expect(__ballot(!ok) != 0, 0)) return ok ? r1 : 1.0f / a;
-    return r1;
-#else
-    return 1.0f / a;
-#endif
-}
-
-// ray_triangle (rt_device.h, Moller-Trumbore scene.cu:160-195) with the reciprocal above.
-__device__ __forceinline__ bool ray_triangle_trace(V3 o, V3 d, V3 p1, V3 e1, V3 e2, float closest, float &t) {
-    const V3 h = cross(d, e2);
-    const float a = dot(h, e1);
-    if (a == 0) return false;
-    const float f = recip(a);
-    const V3 s = o - p1;
-    const float u = dot(s, h) * f;
-    if (u < 0 || u > 1) return false;
-    const V3 q = cross(s, e1);
-    const float v = dot(d, q) * f;
-    if (v < 0 || u + v > 1) return false;
-    t = dot(e2, q) * f;
-    return !(t < kEps || t >= closest);
-}
-
 // Triangle range [ti, te) of a leaf ref (small leaves inline, big ones through big_leaves).
 __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int &ti, int &te) {
     if (ref & kBigLeaf) {
@@ -381,7 +344,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                         o = v3(r0.x, r0.y, r0.z);
                         d = v3(r0.w, r1.x, r1.y);
                     }
-                    ix = recip(d.x); iy = recip(d.y); iz = recip(d.z);
+                    ix = 1 / d.x; iy = 1 / d.y; iz = 1 / d.z;
                     finite_inv = __builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz);
 
                     closest = 1e30f;
@@ -447,7 +410,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             const float q2 = c.x;
             if (COUNT) tt++;
             float t;
-            if (ray_triangle_trace(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t)) {
+            if (ray_triangle(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t)) {
                 closest = t;
                 index = S.sphere_count + ti;
             }
