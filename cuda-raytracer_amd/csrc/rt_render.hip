@@ -242,6 +242,9 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 // do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
 // 8 waves per SIMD (<= 64 VGPRs): the one spill left is a lane constant reloaded only on the
 // overflow-stack path.  +2 % over the unconstrained 66 VGPRs (7 waves).
+#ifndef RT_DEFER_HITS
+#define RT_DEFER_HITS 1               // finished lanes keep their hit in registers until the next refill
+#endif
 #ifndef RT_SEL
 // 1: next/near child chosen by one predicate, the non-finite-1/d check as one ballot per refill instead
 // of one per node step, logical (not bitwise) predicates.  A/B (4 rounds, teapot full frame): 7.50-7.65
@@ -307,6 +310,16 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         unsigned long long idle = __ballot(slot < 0);
         if (!exhausted && __popcll(idle) >= (FIRST ? kRefillFirst : kRefill)) {
             PROF(6, 1);
+#if RT_DEFER_HITS
+            // results of the lanes that finished since the last refill, stored now: on gfx9 a store
+            // counts in vmcnt, so a store issued mid-loop made the next step's vmcnt(0) waits (before
+            // its record loads, before an LDS pop) wait for the write as well; here the stores overlap
+            // the refill's own ray loads
+            if (slot <= -2) {
+                hits[-2 - slot] = make_float2(closest, __int_as_float(index));
+                slot = -1;
+            }
+#endif
             bool fresh = false;
             while (idle && !exhausted) {
                 if (q_next >= q_end) {
@@ -491,8 +504,12 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         while (need) {                  // pop to the next entry nearer than closest
             PROF(10, 1);
             if (sp == 0) {
+#if RT_DEFER_HITS
+                slot = -2 - slot;       // done; {closest, index} stored at the next refill or at exit
+#else
                 hits[slot] = make_float2(closest, __int_as_float(index));
                 slot = -1;
+#endif
                 break;
             }
             sp--;
@@ -519,6 +536,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         asm volatile("" ::"v"(pf));     // keeps the fetch; its wait lands here, after the step's work
 #endif
     }
+#if RT_DEFER_HITS
+    if (slot <= -2) hits[-2 - slot] = make_float2(closest, __int_as_float(index));
+#endif
     Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
     const unsigned long long nl = wave_sum(nlive);
     if (COUNT) {
