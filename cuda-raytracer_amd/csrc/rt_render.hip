@@ -235,23 +235,6 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
     }
 }
 
-// Entering node `ref` when `go` (a descend or an accepted pop): a leaf sets the lane's triangle
-// range; need = the lane must pop again (not entered, or an empty leaf).  The small-leaf decode is
-// plain bit arithmetic and the ranges are committed by selects, so the common path has no branch
-// (and no phi copies of ti/te/ref); only a big leaf's table load branches (RT_POP2).
-__device__ __forceinline__ void enter(const DevScene &S, bool go, uint32_t ref, int &ti, int &te, bool &need) {
-    const bool leaf = go && (ref & kLeaf);
-    int nti = (int)(ref & 0xFFFFFFu), nte = nti + (int)((ref >> 24) & 0x3Fu);
-    if (__builtin_expect(leaf && (ref & kBigLeaf), 0)) {
-        const int2 be = S.big_leaves[ref & 0x3FFFFFFFu];
-        nti = be.x;
-        nte = be.y;
-    }
-    ti = leaf ? nti : ti;
-    te = leaf ? nte : te;
-    need = !go || (leaf && nti == nte);
-}
-
 // Closest hit for the live slots [0, *live): the sphere loop (scene.cu:338-372) and
 // bvh_closest_hit_distance (scene.cu:134-241).  Persistent and wave-refilling: each wave takes
 // chunks of slots from a device queue (one atomic per chunk) and hands a new slot to a lane
@@ -259,9 +242,6 @@ __device__ __forceinline__ void enter(const DevScene &S, bool go, uint32_t ref, 
 // do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
 // 8 waves per SIMD (<= 64 VGPRs): the one spill left is a lane constant reloaded only on the
 // overflow-stack path.  +2 % over the unconstrained 66 VGPRs (7 waves).
-#ifndef RT_POP2
-#define RT_POP2 1                     // branch-free node entry after a descend or a pop (enter())
-#endif
 #ifndef RT_DEFER_HITS
 #define RT_DEFER_HITS 1               // finished lanes keep their hit in registers until the next refill
 #endif
@@ -327,15 +307,8 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 #endif
     while (true) {
         // ---- refill idle lanes (wave-uniform control flow)
-#if RT_SEL
-        // the lanes with a ray, one ballot per iteration (a block is whole waves, so the rest are idle)
-        unsigned long long active = __ballot(slot >= 0);
-        unsigned long long idle = ~active;
-        if (!exhausted && (int)__popcll(idle) >= (FIRST ? kRefillFirst : kRefill)) {
-#else
         unsigned long long idle = __ballot(slot < 0);
         if (!exhausted && __popcll(idle) >= (FIRST ? kRefillFirst : kRefill)) {
-#endif
             PROF(6, 1);
 #if RT_DEFER_HITS
             // results of the lanes that finished since the last refill, stored now: on gfx9 a store
@@ -411,14 +384,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             // one ballot per refill instead of one per node step; the flag stays set until the next
             // refill even if that ray has finished (the per-lane fold below is exact for every lane)
             wave_nonfinite = __ballot(slot >= 0 && !finite_inv) != 0;
-            active = __ballot(slot >= 0);
 #endif
         }
-#if RT_SEL
-        if (!active) {
-#else
         if (!__ballot(slot >= 0)) {
-#endif
             if (exhausted) break;
             PROF(7, 1);
             continue;
@@ -517,10 +485,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 #endif
             ref = any ? next_ref : ref;
             const bool descend = any && !(next_t >= closest);
-#if RT_POP2
-            if (COUNT) pn += descend ? 1u : 0u;
-            enter(S, descend, ref, ti, te, need);
-#else
             need = !descend;
             if (descend) {
                 if (COUNT) pn++;
@@ -529,7 +493,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     need = ti == te;
                 }
             }
-#endif
         }
 #if RT_PREFETCH >= 2
         // ... and the first triangle of a leaf the lane has just entered
@@ -560,13 +523,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 eref = overflow[(sp - kStackLds) * lanes + gl];
                 edist = __uint_as_float(overflow[dist_half + (sp - kStackLds) * lanes + gl]);
             }
-#if RT_POP2
-            const bool take = !(edist >= closest);
-            if (COUNT) pn += take ? 1u : 0u;
-            ref = take ? eref : ref;
-            enter(S, take, ref, ti, te, need);
-            continue;
-#endif
             if (edist >= closest) continue;
             ref = eref;
             if (COUNT) pn++;
