@@ -62,6 +62,9 @@ TILE_ROWS = 8          # pixel-tile stripe height (--shard tiles; SURVEY §8e: i
 
 
 L2_PEAK_GBS = 34500.0  # MI355X aggregate L2 (8 XCDs x 4 MiB), MI355X_MICROARCH.md §L2: ~34.5 TB/s
+# wave64 VALU instruction issue: 256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 instruction
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles"; max clock 2400 MHz)
+VALU_PEAK_GWIS = 256 * 4 * 2.4 / 2
 
 
 def logical_trace_bytes(st, spheres):
@@ -95,6 +98,16 @@ def load_pmc(workload):
     if d:
         d["file"] = "profiles/pmc_traffic.json"
     return d
+
+
+def load_issue(workload):
+    """Wave-instruction counts of one pass from the committed PMC stall run (profiles/pmc_issue.json,
+    tools/pmc.sh ... stall.txt + tools/stall_summary.py --json)."""
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_issue.json")) as f:
+            return json.load(f).get(workload)
+    except (OSError, ValueError):
+        return None
 
 
 def load_golden(scene, sort):
@@ -408,6 +421,17 @@ def main():
                                  "frac": round(pmc["pass_bytes"] / (ms_pass / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                  "def": "measured HBM-side bytes of one pass (every kernel, same PMC run) / timed "
                                         "wall per pass (one GPU's passes overlap 20 at a time)"}
+            iss = load_issue(workload)
+            if iss and steps:
+                ms_pass = elapsed / steps * 1e3
+                v_all, v_tr = iss["per_pass"]["SQ_INSTS_VALU"], iss["trace_per_pass"]["SQ_INSTS_VALU"]
+                rate = v_all / (ms_pass / 1e3) / 1e9
+                roof["valu"] = {"wave_instructions_per_pass": int(v_all), "trace_share": round(v_tr / v_all, 3),
+                                "achieved": round(rate, 1), "peak": VALU_PEAK_GWIS, "unit": "G wave64 VALU instr/s",
+                                "frac": round(rate / VALU_PEAK_GWIS, 4),
+                                "def": "VALU wave-instructions of one pass, every kernel (rocprofv3 --pmc SQ_INSTS_VALU, "
+                                       "profiles/pmc_issue.json: %s) / timed wall per pass, against the chip's issue "
+                                       "rate (1024 SIMD-32 x 2.4 GHz / 2 cycles)" % iss.get("run", "")}
         value = live / elapsed / 1e6 if elapsed > 0 else 0.0
         nominal = gen * bounces / elapsed / 1e6 if elapsed > 0 else 0.0
         ms_step = elapsed / steps * 1e3 if steps else 0.0

@@ -2,7 +2,8 @@
 # Round measurement on the GPU box, in two parts (each GPU step under its own time limit; stops at
 # the first failure).  Outputs under gpurun_out/TAG/; copy what is judged into profiles/rNN/.
 #   part A: GPU test suite, smoke(), PMC passes of one profiled teapot pass (traffic -> summarised into
-#           profiles/pmc_traffic.json, which the bench reads for roofline.traffic; stall; trace), the
+#           profiles/pmc_traffic.json, which the bench reads for roofline.traffic; stall -> instruction
+#           counts in profiles/pmc_issue.json, read for roofline.valu; trace), the
 #           headline bench line, the driver-style --steps 20 line, rocprofv3 kernel-trace summary.
 #   part B: bench lines of the other BASELINE configs, the strong-scaling probe, REPORT.pdf Table 1.
 # usage: tools/round_measure.sh TAG A|B
@@ -27,7 +28,10 @@ if [ "$PART" = A ]; then
   cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
   step pmc stall + trace
   bash tools/pmc.sh ${TAG}_st tools/pmc_groups/stall.txt > $OUT/pmc_st.log 2>&1 || { cat $OUT/pmc_st.log; exit 1; }
-  python3 tools/stall_summary.py ${TAG}_st > $OUT/pmc_stall_teapot.txt || exit 1
+  python3 tools/stall_summary.py ${TAG}_st --json profiles/pmc_issue.json \
+      --workload "teapot.scene 1920x1080 2048spp 16 bounces sort=on" \
+      --run "rev $REV: python3 bench.py --steps 1 --warmup 0 --no-extras (tools/pmc.sh ${TAG}_st)" > $OUT/pmc_stall_teapot.txt || exit 1
+  cp profiles/pmc_issue.json $OUT/pmc_issue.json
   bash tools/pmc.sh ${TAG}_tr tools/pmc_groups/trace.txt > $OUT/pmc_trc.log 2>&1 || { cat $OUT/pmc_trc.log; exit 1; }
   python3 tools/pmc_summary.py ${TAG}_tr > $OUT/pmc_trace_teapot.txt || exit 1
   step bench teapot
