@@ -33,8 +33,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -70,6 +73,46 @@ struct DevState {
     double exchange_ms = 0;
 };
 
+// A device that fails must not leave its peers blocked in a collective.  Every device first builds
+// its renderer and buffers (where nearly every failure happens: out of memory, a bad scene) and
+// meets the others; if any failed, all return before the first collective.  A failure after that
+// aborts every communicator, which ends the peers' pending collectives with an error.
+struct Sync {
+    std::mutex m;
+    std::condition_variable cv;
+    int world = 0, arrived = 0;
+    bool failed = false;
+    std::vector<ncclComm_t> *comms = nullptr;
+    std::atomic<bool> aborted{false};
+    bool setup_done(bool ok) {   // false if any device's setup failed
+        std::unique_lock<std::mutex> l(m);
+        if (!ok) failed = true;
+        if (++arrived == world) cv.notify_all();
+        else cv.wait(l, [&] { return arrived == world; });
+        return !failed;
+    }
+    void abort() {
+        bool expected = false;
+        if (aborted.compare_exchange_strong(expected, true))
+            for (ncclComm_t c : *comms) (void)ncclCommAbort(c);
+    }
+};
+
+// Scope guard of one device's run: arrives at the setup barrier as failed if the run ends before
+// setup(), and aborts the communicators if it ends with an error after it.
+struct RunGuard {
+    Sync &sy;
+    bool arrived = false, ok = false;
+    bool setup() {
+        arrived = true;
+        return sy.setup_done(true);
+    }
+    ~RunGuard() {
+        if (!arrived) (void)sy.setup_done(false);
+        else if (!ok) sy.abort();
+    }
+};
+
 int hip_err(hipError_t e, const char *what) {
     return rtamd::fail(e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP,
                        std::string("Error ") + what + " " + hipGetErrorString(e));
@@ -92,7 +135,8 @@ namespace {
 
 // Device `st.rank`'s share of the frame: render, exchange, add; the root also gathers.
 int run_device(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int world, DevState &st,
-               float *fb_out) {
+               float *fb_out, Sync &sy) {
+    RunGuard run{sy};
     MHIP(hipSetDevice(st.device));
     const int P = (scene->ray_count + 19) / 20;
     const size_t px3 = (size_t)scene->width * scene->height * 3;
@@ -131,6 +175,7 @@ int run_device(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int 
     MHIP(hipMemsetAsync(buf, 0, (size_t)chunk * pitch * sizeof(float), g.s));   // padding stays 0
     MHIP(hipMemsetAsync(slice, 0, sl * sizeof(float), g.s));
     MHIP(hipStreamSynchronize(g.s));
+    if (!run.setup()) return rtamd::fail(RT_E_INVALID, "another device of the render failed");
     using clk = std::chrono::high_resolution_clock;
     for (int k0 = 0; k0 < R; k0 += chunk) {
         const int m = std::min(chunk, R - k0);
@@ -179,6 +224,7 @@ int run_device(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int 
     if (st.rank == 0) MHIP(hipMemcpyAsync(fb_out, slice, px3 * sizeof(float), hipMemcpyDeviceToHost, g.s));
     MHIP(hipStreamSynchronize(g.s));
     st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    run.ok = true;
     return RT_OK;
 }
 
@@ -194,7 +240,8 @@ int nccl_exchange(void *user, uint8_t *bytes, uint64_t n, void *stream) {
 // ncclReduce of the owners' framebuffers to the root: every pixel has one owner and is 0 elsewhere,
 // so the sum is that owner's value bit for bit (x + 0 = x).
 int run_device_tiles(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int world, DevState &st,
-                     float *fb_out) {
+                     float *fb_out, Sync &sy) {
+    RunGuard run{sy};
     MHIP(hipSetDevice(st.device));
     const size_t px3 = (size_t)scene->width * scene->height * 3;
     rt_opts o = *base;
@@ -224,13 +271,14 @@ int run_device_tiles(const rt_scene *scene, const rt_opts *base, ncclComm_t comm
         rc = rt_renderer_set_exchange(ren, nccl_exchange, &comm, 1);
         if (rc) return rc;
     }
+    MHIP(hipMalloc(reinterpret_cast<void **>(&g.d), px3 * sizeof(float)));
+    MHIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
+    if (!run.setup()) return rtamd::fail(RT_E_INVALID, "another device of the render failed");
     rt_stats s{};
     using clk = std::chrono::high_resolution_clock;
     rc = rtamd_renderer_run_pitched(ren, 0, -1, 1, nullptr, 0, &s);
     if (rc) return rc;
     st.stats = s;
-    MHIP(hipMalloc(reinterpret_cast<void **>(&g.d), px3 * sizeof(float)));
-    MHIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
     rc = rt_renderer_copy_framebuffer(ren, g.d);
     if (rc) return rc;
     const auto t0 = clk::now();
@@ -238,6 +286,7 @@ int run_device_tiles(const rt_scene *scene, const rt_opts *base, ncclComm_t comm
     if (st.rank == 0) MHIP(hipMemcpyAsync(fb_out, g.d, px3 * sizeof(float), hipMemcpyDeviceToHost, g.s));
     MHIP(hipStreamSynchronize(g.s));
     st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    run.ok = true;
     return RT_OK;
 }
 
@@ -264,18 +313,25 @@ int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out
     std::vector<ncclComm_t> comms(world);
     MNCCL(ncclCommInitAll(comms.data(), world, devs.data()));
     std::vector<DevState> st(world);
+    Sync sy;
+    sy.world = world;
+    sy.comms = &comms;
     std::vector<std::thread> th;
     for (int k = 0; k < world; k++) {
         st[k].device = devs[k];
         st[k].rank = k;
         th.emplace_back([&, k]() {
-            st[k].rc = opts->shard_tiles ? run_device_tiles(scene, opts, comms[k], world, st[k], fb_out)
-                                         : run_device(scene, opts, comms[k], world, st[k], fb_out);
+            st[k].rc = opts->shard_tiles ? run_device_tiles(scene, opts, comms[k], world, st[k], fb_out, sy)
+                                         : run_device(scene, opts, comms[k], world, st[k], fb_out, sy);
             if (st[k].rc) st[k].err = rt_last_error();
         });
     }
     for (auto &t : th) t.join();
-    for (auto c : comms) (void)ncclCommDestroy(c);
+    if (!sy.aborted)    // ncclCommAbort already freed them
+        for (auto c : comms) (void)ncclCommDestroy(c);
+    // report the device that failed first-hand, not a peer that returned because of it
+    for (auto &s : st)
+        if (s.rc && s.err.find("another device") == std::string::npos) return rtamd::fail(s.rc, s.err);
     for (auto &s : st)
         if (s.rc) return rtamd::fail(s.rc, s.err);
     if (stats) {
