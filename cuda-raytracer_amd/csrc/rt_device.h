@@ -106,23 +106,6 @@ RT_HD uint32_t quant_bit(float v) {
     return (uint32_t)q & 1u;
 }
 RT_HD uint32_t bucket_of(V3 o, V3 d, V3 min_coord, V3 inv_dim) {
-#if defined(RT_EXPERIMENT_KEY) && !defined(RT_HOST_CPU_PATH)
-    // MEASUREMENT ONLY (breaks parity): a coherence key instead of the reference's parity bits,
-    // to size what grouping rays by direction/origin would buy the traversal
-    {
-        const V3 a = (o - min_coord) * inv_dim;
-        const uint32_t dx = d.x < 0, dy = d.y < 0, dz = d.z < 0;
-#if RT_EXPERIMENT_KEY == 1
-        return (dz << 5) | (dy << 4) | (dx << 3) | ((a.z > 0.5f) << 2) | ((a.y > 0.5f) << 1) | (uint32_t)(a.x > 0.5f);
-#else
-        const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-        const uint32_t dom = (ax >= ay && ax >= az) ? 0u : (ay >= az ? 1u : 2u);
-        const float m = dom == 0 ? ax : (dom == 1 ? ay : az);
-        const float o1 = dom == 0 ? ay : ax, o2 = dom == 2 ? ay : az;
-        return (dz << 5) | (dy << 4) | (dx << 3) | (dom << 1) | (uint32_t)(fmaxf(o1, o2) > 0.5f * m);
-#endif
-    }
-#endif
     const V3 a = (o - min_coord) * inv_dim;
     const V3 b = 0.5f * (d + v3(1, 1, 1));
     return (quant_bit(a.z) << 5) | (quant_bit(a.y) << 4) | (quant_bit(a.x) << 3) |

@@ -242,18 +242,6 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 // do not leave most lanes idle.  Output per slot: {closest t, hit index} (index -1 = miss).
 // 8 waves per SIMD (<= 64 VGPRs): the one spill left is a lane constant reloaded only on the
 // overflow-stack path.  +2 % over the unconstrained 66 VGPRs (7 waves).
-#ifndef RT_DEFER_HITS
-#define RT_DEFER_HITS 1               // finished lanes keep their hit in registers until the next refill
-#endif
-#ifndef RT_SEL
-// 1: next/near child chosen by one predicate, the non-finite-1/d check as one ballot per refill instead
-// of one per node step, logical (not bitwise) predicates.  A/B (4 rounds, teapot full frame): 7.50-7.65
-// -> 7.28-7.37 ms/pass; 20 steps 7.87 -> 7.67.  0 keeps the round-1 step for A/B.
-#define RT_SEL 1
-#endif
-#ifndef RT_PREFETCH
-#define RT_PREFETCH 0                 // 1: fetch an internal node's child-pair line during its slab tests; 2: + leaf
-#endif
 #ifndef RT_TRACE_WPE
 #define RT_TRACE_WPE 8
 #endif
@@ -295,9 +283,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     V3 o{0, 0, 0}, d{0, 0, 0};
     float ix = 0, iy = 0, iz = 0, closest = 0;
     bool finite_inv = true;
-#if RT_SEL
     bool wave_nonfinite = false;        // some lane's ray has an infinite 1/d component (set at refill)
-#endif
     int index = -1, sp = 0;
     uint32_t ref = 0;
     int ti = 0, te = 0;                 // the lane is in a leaf while ti < te
@@ -310,16 +296,14 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         unsigned long long idle = __ballot(slot < 0);
         if (!exhausted && __popcll(idle) >= (FIRST ? kRefillFirst : kRefill)) {
             PROF(6, 1);
-#if RT_DEFER_HITS
-            // results of the lanes that finished since the last refill, stored now: on gfx9 a store
-            // counts in vmcnt, so a store issued mid-loop made the next step's vmcnt(0) waits (before
-            // its record loads, before an LDS pop) wait for the write as well; here the stores overlap
-            // the refill's own ray loads
+            // results of the lanes that finished since the last refill (slot -2 - s: done with slot s),
+            // stored now: on gfx9 a store counts in vmcnt, so a store issued mid-loop made the next
+            // step's vmcnt(0) waits (before its record loads, before an LDS pop) wait for the write as
+            // well; here the stores overlap the refill's own ray loads (A/B 7.13 -> 7.00 ms/pass)
             if (slot <= -2) {
                 hits[-2 - slot] = make_float2(closest, __int_as_float(index));
                 slot = -1;
             }
-#endif
             bool fresh = false;
             while (idle && !exhausted) {
                 if (q_next >= q_end) {
@@ -380,11 +364,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     }
                 }
             }
-#if RT_SEL
             // one ballot per refill instead of one per node step; the flag stays set until the next
             // refill even if that ray has finished (the per-lane fold below is exact for every lane)
             wave_nonfinite = __ballot(slot >= 0 && !finite_inv) != 0;
-#endif
         }
         if (!__ballot(slot >= 0)) {
             if (exhausted) break;
@@ -411,9 +393,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         // node's interleaved child bounds and child refs), issued before the branch, so a step
         // costs one memory round trip whatever mix of leaf and internal lanes the wave holds.
         bool need = false;              // the lane needs the next node from its stack
-#if RT_PREFETCH
-        float pf = 0.0f;                // line fetched ahead for the next step (consumed at the step's end)
-#endif
         const bool in_leaf = ti < te;
         const float4 *rec = in_leaf ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4;
         const float4 a = rec[0], b = rec[1], c = rec[2];
@@ -430,22 +409,10 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             need = ++ti == te;
         } else {
             if (COUNT) iv++;
-#if RT_PREFETCH
-            // the children's records are siblings (one 128-B line): fetch the line while the slabs
-            // run, so the next step's record load finds it in L1/L2 when the lane descends
-            {
-                const uint32_t kin = (kids.x & kLeaf) ? kids.y : kids.x;
-                if (!(kin & kLeaf)) pf = S.nodes[(size_t)kin * 4].x;
-            }
-#endif
             float t0, t1;
             bool h0, h1;
             slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
-#if RT_SEL
             if (__builtin_expect(wave_nonfinite, 0)) {
-#else
-            if (__builtin_expect(__ballot(!finite_inv) != 0, 0)) {
-#endif
                 // some lane's 1/d has an infinite component (0 * inf may give NaN): the literal
                 // per-axis fold for those lanes
                 float u0, u1;
@@ -456,21 +423,14 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             // The reference pushes the hit children near then far (scene.cu:204-225) and pops the
             // top: with both hit the far child is next and the near one stays on the stack; with
             // one hit that one is next.  Next is entered unless its entry distance >= closest.
-#if RT_SEL
+            // (one predicate picks both children, logical not bitwise predicates: A/B 7.50-7.65 ->
+            // 7.28-7.37 ms/pass with the refill-time non-finite ballot above)
             const bool both = h0 && h1, any = h0 || h1;
             // next = child 1 iff it is the far child of two hits (t0 < t1; a tie makes child 1 the
             // near one) or the only hit; the other child is the near one, pushed when both hit
             const bool sel1 = h1 && (!h0 || t0 < t1);
             const uint32_t next_ref = sel1 ? kids.y : kids.x, near_ref = sel1 ? kids.x : kids.y;
             const float next_t = sel1 ? t1 : t0, near_t = sel1 ? t0 : t1;
-#else
-            const bool both = h0 & h1, any = h0 | h1;
-            const bool x_near = t0 < t1;
-            const uint32_t near_ref = x_near ? kids.x : kids.y, far_ref = x_near ? kids.y : kids.x;
-            const float near_t = x_near ? t0 : t1, far_t = x_near ? t1 : t0;
-            const uint32_t next_ref = both ? far_ref : (h0 ? kids.x : kids.y);
-            const float next_t = both ? far_t : (h0 ? t0 : t1);
-#endif
             // the near child is written either way (above the top when not pushed; entry
             // kStackLds is a scratch slot), so the push needs no branch
             col[min(sp, kStackLds) * kBlock] = make_uint2(near_ref, __float_as_uint(near_t));
@@ -478,11 +438,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 overflow[(sp - kStackLds) * lanes + gl] = near_ref;
                 overflow[dist_half + (sp - kStackLds) * lanes + gl] = __float_as_uint(near_t);
             }
-#if RT_SEL
             if (both) sp++;
-#else
-            sp += both ? 1 : 0;
-#endif
             ref = any ? next_ref : ref;
             const bool descend = any && !(next_t >= closest);
             need = !descend;
@@ -494,22 +450,13 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 }
             }
         }
-#if RT_PREFETCH >= 2
-        // ... and the first triangle of a leaf the lane has just entered
-        if (ti < te && !in_leaf) pf += S.tris[(size_t)ti * 3].x;
-#endif
 #ifdef RT_PROFILE
         if (__ballot(need)) PROF(5, 1);
 #endif
         while (need) {                  // pop to the next entry nearer than closest
             PROF(10, 1);
             if (sp == 0) {
-#if RT_DEFER_HITS
                 slot = -2 - slot;       // done; {closest, index} stored at the next refill or at exit
-#else
-                hits[slot] = make_float2(closest, __int_as_float(index));
-                slot = -1;
-#endif
                 break;
             }
             sp--;
@@ -532,13 +479,8 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 need = ti == te;
             }
         }
-#if RT_PREFETCH
-        asm volatile("" ::"v"(pf));     // keeps the fetch; its wait lands here, after the step's work
-#endif
     }
-#if RT_DEFER_HITS
     if (slot <= -2) hits[-2 - slot] = make_float2(closest, __int_as_float(index));
-#endif
     Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
     const unsigned long long nl = wave_sum(nlive);
     if (COUNT) {
@@ -1209,7 +1151,6 @@ struct rt_renderer {
     PassCtx ctx[kInflight];
     int pass_hint = 0;                // rt_render: the passes this renderer will ever run (0: any)
     int trace_blocks = 0;             // persistent trace_kernel grid of the current run
-    int trace_blocks_heavy = 0;       // ... for bounces 0 and 1
     int trace_blocks_max = 0;         // all resident trace workgroups (the overflow stacks are sized for it)
     int nctx = 1;                     // pass contexts allocated (passes in flight)
     int cus = 0;
@@ -1442,7 +1383,7 @@ struct rt_renderer {
         const int n = (int)(rtc * tpix);
         const int grid = blocks_for(n);
         const int tiles = (n + kSortTile - 1) / kSortTile;
-        int tgrid = std::min(grid, trace_blocks);
+        const int tgrid = std::min(grid, trace_blocks);
         const int sgrid = std::min(grid, cus * RT_SHADE_BPC);
         // tile-stride reorder kernels on at most 8 blocks per CU: in the tail bounces a block per
         // possible tile dispatched ~10^4 empty workgroups per launch (A/B: +0.3-0.5 %)
@@ -1477,7 +1418,6 @@ struct rt_renderer {
             const uint32_t *lv = c.live.p + b;
             uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
             const bool last = b + 1 == bounces;
-            tgrid = std::min(grid, b <= 1 ? trace_blocks_heavy : trace_blocks);
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
@@ -1780,11 +1720,6 @@ struct rt_renderer {
             const int pct = kTraceOccPct > 0 ? kTraceOccPct
                                              : std::min(100, std::max(RT_TRACE_OCC_MIN, 200 / concurrent));
             trace_blocks = std::max(1, trace_blocks_max * pct / 100);
-            // RTAMD_TRACE_HEAVY (A/B knob): % of the resident workgroups for the bounce-0/1 launches,
-            // which hold nearly every ray of a pass (0: the same grid as the tail bounces)
-            const char *h = std::getenv("RTAMD_TRACE_HEAVY");
-            const int hp = h ? std::atoi(h) : 0;
-            trace_blocks_heavy = hp > 0 ? std::max(1, trace_blocks_max * std::min(100, hp) / 100) : trace_blocks;
         }
         hipStream_t s0 = stream();
         if (pass_events && tspans.n < (size_t)std::max(count, 1) * 2 * (bounces + 1)) {
