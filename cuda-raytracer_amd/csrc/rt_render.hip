@@ -1599,7 +1599,12 @@ struct rt_renderer {
                 HIPCHK(hipMemcpyAsync(xhost, c.gbytes.p, lg, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
                 rc = xfn(xuser, xhost, lg, st);
-                if (!rc) HIPCHK(hipMemcpyAsync(c.gbytes.p, xhost, lg, hipMemcpyHostToDevice, st));
+                if (!rc) {
+                    HIPCHK(hipMemcpyAsync(c.gbytes.p, xhost, lg, hipMemcpyHostToDevice, st));
+                    // xhost is shared by the passes in flight: the next pass's bytes overwrite it, so
+                    // this copy must have read it first
+                    HIPCHK(hipStreamSynchronize(st));
+                }
             }
             if (rc) return rtamd::fail(RT_E_INVALID, "tile exchange callback failed (" + std::to_string(rc) + ")");
         }
