@@ -185,8 +185,8 @@ def main():
                     help="only the warmup and timed steps (profiling: --steps 1 --warmup 0 renders exactly one pass)")
     ap.add_argument("--dist", action="store_true", help="use the torch.distributed path even at N=1")
     ap.add_argument("--shard", choices=("passes", "tiles"), default="passes",
-                    help="multi-GPU decomposition: whole passes per GPU (exact in both sort modes) or "
-                         "8-row pixel stripes per GPU over every pass (exact with --no-sort only)")
+                    help="multi-GPU decomposition: whole passes per GPU or 8-row pixel stripes per GPU over "
+                         "every pass (sort on: one byte per live ray all-reduced after every bounce); both exact")
     ap.add_argument("--tile-share", type=int, default=0, metavar="N",
                     help="1-GPU probe of --shard tiles: render only rank 0's stripes of an N-GPU split")
     args = ap.parse_args()
