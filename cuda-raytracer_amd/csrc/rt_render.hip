@@ -758,7 +758,8 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
     __syncthreads();
     const int wave = threadIdx.x >> 6;
     const int base = tile * kSortTile;
-    for (int r = 0; r < kSortItems; r++) {
+    const int rounds = min(kSortItems, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
+    for (int r = 0; r < rounds; r++) {
         const int item = base + r * kBlock + threadIdx.x;
         const bool valid = item < n;
         const uint32_t b = valid ? bkt_in[item] : 0u;
@@ -849,7 +850,8 @@ __global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__rest
         __syncthreads();
         const int wave = threadIdx.x >> 6;
         const int base = tile * kSortTile;
-        for (int r = 0; r < kSortItems; r++) {
+        const int rounds = min(kSortItems, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
+        for (int r = 0; r < rounds; r++) {
             const int item = base + r * kBlock + threadIdx.x;
             const bool valid = item < n;
             const uint32_t b = valid ? bkt_in[item] : 0u;
@@ -908,7 +910,8 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
         __syncthreads();
         const int wave = threadIdx.x >> 6;
         const int base = tile * kSortTile;
-        for (int r = 0; r < kSortItems; r++) {
+        const int rounds = min(kSortItems, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
+        for (int r = 0; r < rounds; r++) {
             const int item = base + r * kBlock + threadIdx.x;
             const bool valid = item < n;
             const uint32_t b = valid ? bkt_in[item] : 0u;
