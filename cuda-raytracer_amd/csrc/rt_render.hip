@@ -658,6 +658,26 @@ __device__ __forceinline__ unsigned long long match_bucket(uint32_t b, bool vali
     return peers;
 }
 
+// run[b] = the pass's live rays in buckets < b + bucket b's rays in tiles before `tile`: the first
+// wave loads the totals and offsets of the 65 buckets at once and prefix-sums the totals with a
+// wave scan (one thread walking the buckets paid ~65 dependent scalar loads per tile).
+__device__ __forceinline__ void bucket_runs(uint32_t *run, const uint32_t *__restrict__ offsets,
+                                            const uint32_t *__restrict__ totals, int tiles, int tile) {
+    static_assert(kBuckets == 65 && kDead == 64, "buckets 0..63 in one wave, the terminated bucket after them");
+    if (threadIdx.x < 64) {
+        const int b = (int)threadIdx.x;
+        const uint32_t t = totals[b];
+        uint32_t x = t;                 // inclusive scan of the totals over the wave
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (b >= off) x += y;
+        }
+        run[b] = x - t + offsets[(size_t)b * tiles + tile];
+        if (b == 63) run[kDead] = x + offsets[(size_t)kDead * tiles + tile];
+    }
+}
+
 // Per-tile bucket counts, written bucket-major: counts[b * tiles + tile].
 __global__ __launch_bounds__(kBlock) void sort_hist_kernel(const uint8_t *__restrict__ bkt,
                                                            const uint32_t *__restrict__ live_count, int tiles,
@@ -672,6 +692,7 @@ __global__ __launch_bounds__(kBlock) void sort_hist_kernel(const uint8_t *__rest
         const int base = tile * kSortTile;
 #pragma unroll 4
         for (int r = 0; r < kSortItems; r++) {
+            if (base + r * kBlock >= n) break;   // block-uniform: the live prefix's last tile is short
             const int item = base + r * kBlock + threadIdx.x;
             const bool valid = item < n;
             const uint32_t b = valid ? bkt[item] : 0u;
@@ -747,13 +768,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
     for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {   // tile-stride (capped grid)
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int b = 0; b < kBuckets; b++) {
-            run[b] = acc + offsets[(size_t)b * tiles + tile];
-            acc += totals[b];
-        }
-    }
+    bucket_runs(run, offsets, totals, tiles, tile);
     for (int k = threadIdx.x; k < (kBlock / 64) * kBuckets; k += kBlock) (&wcount[0][0])[k] = 0;
     __syncthreads();
     const int wave = threadIdx.x >> 6;
@@ -839,13 +854,7 @@ __global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__rest
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
     for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0;
-            for (int b = 0; b < kBuckets; b++) {
-                run[b] = acc + offsets[(size_t)b * tiles + tile];
-                acc += totals[b];
-            }
-        }
+        bucket_runs(run, offsets, totals, tiles, tile);
         for (int k = threadIdx.x; k < (kBlock / 64) * kBuckets; k += kBlock) (&wcount[0][0])[k] = 0;
         __syncthreads();
         const int wave = threadIdx.x >> 6;
@@ -899,13 +908,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
     for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0;
-            for (int b = 0; b < kBuckets; b++) {
-                run[b] = acc + offsets[(size_t)b * tiles + tile];
-                acc += totals[b];
-            }
-        }
+        bucket_runs(run, offsets, totals, tiles, tile);
         for (int k = threadIdx.x; k < (kBlock / 64) * kBuckets; k += kBlock) (&wcount[0][0])[k] = 0;
         __syncthreads();
         const int wave = threadIdx.x >> 6;
