@@ -5,7 +5,8 @@
 #           profiles/pmc_traffic.json, which the bench reads for roofline.traffic; stall -> instruction
 #           counts in profiles/pmc_issue.json, read for roofline.valu; trace), the
 #           headline bench line, the driver-style --steps 20 line, rocprofv3 kernel-trace summary.
-#   part B: bench lines of the other BASELINE configs, the strong-scaling probe, REPORT.pdf Table 1.
+#   part B: bench lines of the other BASELINE configs, the strong-scaling probe, REPORT.pdf Table 1
+#           (their PMC records come from tools/pmc_configs.sh, run before part B).
 # usage: tools/round_measure.sh TAG A|B
 TAG=$1; PART=$2
 export TMPDIR=/tmp
