@@ -75,14 +75,17 @@ def logical_trace_bytes(st, spheres):
             64 * st["internal_visits"] + 48 * st["triangle_tests"])
 
 
-def compulsory_trace_bytes(st, scene_bytes, launches):
+XCDS = 8   # MI355X: 8 XCDs, each with its own non-coherent 4 MB L2 (MI355X_MICROARCH.md)
+
+
+def compulsory_trace_bytes(st, scene_bytes, launches, per_xcd=False):
     """Algorithmic HBM bytes of the trace launches: what a launch cannot avoid moving from or to
     HBM.  Each live segment's ray (o, d: 24 B) is read once, except at bounce 0 where the primary
     ray is computed in place (every generated ray is live there); its hit {t, index} (8 B) is
     written once; the scene's node and triangle arrays (reference layouts, 32 B / 48 B / 16 B per
-    sphere) are read once per launch."""
+    sphere) are read once per launch, or once per XCD (per_xcd: every XCD's L2 fetches them)."""
     live, gen = st["live_segments"], st["generated_rays"]
-    return 24 * (live - gen) + 8 * live + launches * scene_bytes
+    return 24 * (live - gen) + 8 * live + launches * scene_bytes * (XCDS if per_xcd else 1)
 
 
 def load_pmc(workload):
@@ -138,9 +141,12 @@ def cpu_baseline(cfg, args):
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
     nproc = os.cpu_count() or 1
-    # the GPU pool sets OMP_NUM_THREADS to the box's CPU share for one GPU (16); elsewhere: nproc
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    # The GPU pool sets OMP_NUM_THREADS to the box's CPU share for one GPU (16) and asks jobs to size
+    # worker pools to it, although the affinity mask shows the whole host (256): the baseline runs on
+    # that share.  Elsewhere (no OMP_NUM_THREADS): every thread of the affinity mask.
     env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = args.cpu_threads or env_threads or nproc
+    threads = args.cpu_threads or env_threads or affinity
     scene, w, h, spp, bounces = cfg[:5]
     P = -(-spp // 20)
     if P <= 4:
@@ -165,9 +171,119 @@ def cpu_baseline(cfg, args):
         "frame_s": round(secs, 3),
         "extrapolated": P > 4,
         "host_nproc": nproc,
-        "threads_from": "--cpu-threads" if args.cpu_threads else ("OMP_NUM_THREADS (the pool's CPU share per GPU)"
-                                                                  if env_threads else "nproc"),
+        "affinity_threads": affinity,
+        "threads_from": "--cpu-threads" if args.cpu_threads else ("OMP_NUM_THREADS (the pool's CPU share per GPU; "
+                                                                  "the affinity mask allows %d)" % affinity
+                                                                  if env_threads else "the affinity mask"),
     }
+
+
+def exclusive_pass(scene, sort, device):
+    """Pass 0 alone on the chip (untimed): a renderer with one pass context (RTAMD_INFLIGHT=1, so its
+    trace grid is every resident workgroup), per-launch device wall-clock spans of its trace launches
+    (rt_stats.trace_ms / trace_launches, event timing on), then the same pass with the work
+    counters.  This is the exclusive launch duration the dominant kernel's roofline is priced on,
+    the same serialised situation as the rocprofv3 --pmc pass (tools/pmc.sh: one pass, dispatches
+    serialised by the profiler)."""
+    old = os.environ.get("RTAMD_INFLIGHT")
+    os.environ["RTAMD_INFLIGHT"] = "1"
+    try:
+        r1 = rtamd.Renderer(scene, sort=sort, device=device)
+    finally:
+        if old is None:
+            del os.environ["RTAMD_INFLIGHT"]
+        else:
+            os.environ["RTAMD_INFLIGHT"] = old
+    try:
+        r1.set_event_timing(True)
+        r1.run(0, 1)                        # warm
+        runs = [r1.run(0, 1) for _ in range(3)]
+        best = min(runs, key=lambda st: st["trace_ms"])
+        r1.set_counters(True)
+        counted = r1.run(0, 1)
+        r1.set_counters(False)
+    finally:
+        r1.close()
+    n = best["trace_launches"]
+    return {"trace_ms": best["trace_ms"], "launches": n, "ms_per_launch": best["trace_ms"] / n if n else 0.0,
+            "kernel_ms": best["kernel_ms"], "counted": {k: int(v) for k, v in counted.items() if isinstance(v, int)}}
+
+
+def roofline(excl, counted, launches, trace_ms, scene_bytes, spheres, workload, elapsed, steps):
+    """The dominant kernel (trace_kernel) against HBM, per launch, reproducible from committed files:
+    achieved = algorithmic bytes / exclusive launch duration; traffic = rocprofv3 --pmc fabric bytes
+    of the same serialised pass (profiles/pmc_traffic.json, with the profiler's own per-launch
+    durations beside them).  The timed region's shared-chip spans are a labelled secondary field."""
+    xc = excl["counted"]
+    n_ex = excl["launches"]
+    ms_ex = excl["ms_per_launch"]
+    comp_ex = compulsory_trace_bytes(xc, scene_bytes, n_ex, per_xcd=True) / n_ex
+    logical_ex = logical_trace_bytes(xc, spheres) / n_ex
+    achieved = comp_ex / (ms_ex / 1e3) / 1e9
+    pmc = load_pmc(workload)
+    traffic = pmc["trace_bytes_per_launch"] if pmc else None
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "trace_kernel (BVH traversal + Moller-Trumbore + slab + sphere loop), per launch",
+            "bytes_per_launch": int(comp_ex), "ms_per_launch": round(ms_ex, 4), "launches": n_ex,
+            "achieved_def": "algorithmic HBM bytes per trace launch of pass 0 run alone on the chip (24 B ray read "
+                            "per live segment past bounce 0 + 8 B hit write per live segment + the scene's node and "
+                            "triangle arrays (reference layouts, 32 / 48 B) once per XCD: 8 non-coherent 4 MB L2s each "
+                            "fetch the scene) / its exclusive average launch duration (device wall clock, first wave "
+                            "start to last wave end, one pass context, trace grid = every resident workgroup, best "
+                            "of 3; bench.py exclusive_pass)",
+            "traffic_def": None if not pmc else
+            "measured fabric-side bytes per trace launch, rocprofv3 --pmc over exactly pass 0 with dispatches "
+            "serialised (%s; reads priced by request size TCC_EA0_RDREQ_{128B,64B,32B}, = 2 x FETCH_SIZE for 128-B "
+            "requests per MI355X_MICROARCH.md §HBM; writes TCC_EA0_WRREQ{,_64B}; Infinity-Cache hits included, "
+            "an upper bound on HBM bytes); %s" % (pmc["file"], pmc.get("run", "")),
+            "traffic_frac": round(traffic / (ms_ex / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+            "traffic_over_algorithmic": round(traffic / comp_ex, 3) if traffic else None}
+    if pmc and pmc.get("trace_dur_ms_avg"):
+        roof["pmc_run"] = {"ms_per_launch": round(pmc["trace_dur_ms_avg"], 4),
+                           "fabric_gbs": round(pmc["trace_fabric_gbs"], 1),
+                           "frac": round(pmc["trace_fabric_gbs"] / HBM_PEAK_GBS, 4),
+                           "def": "the PMC run's own numbers: fabric bytes per trace launch / the profiler's average "
+                                  "trace dispatch duration (profiles/pmc_traffic.json trace_dur_ms_per_launch)"}
+    comp_sh = compulsory_trace_bytes(counted, scene_bytes, launches, per_xcd=True) / launches
+    roof["shared"] = {"ms_per_launch": round(trace_ms, 4), "launches": launches,
+                      "achieved": round(comp_sh / (trace_ms / 1e3) / 1e9, 1),
+                      "frac": round(comp_sh / (trace_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "def": "secondary: the timed steps' trace launches, re-run untimed with event timing; up to 20 "
+                             "passes share the chip, so a launch's span includes time it shared (what rocprofv3's "
+                             "kernel trace of the bench command reports as the average trace duration)"}
+    roof["l2"] = {"achieved": round(logical_ex / (ms_ex / 1e3) / 1e9, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(logical_ex / (ms_ex / 1e3) / 1e9 / L2_PEAK_GBS, 4), "bytes_per_launch": int(logical_ex),
+                  "def": "SURVEY.md 8(d) logical cache-inclusive bytes of the traversal (24 B ray + 16 B x S + 32 B x "
+                         "node pops + 64 B x internal visits + 48 B x triangle tests + 8 B hit) per exclusive launch / "
+                         "its duration, against the aggregate L2 rate (MI355X_MICROARCH.md §L2)"}
+    if steps and elapsed > 0:
+        ms_pass = elapsed / steps * 1e3
+        lg = logical_trace_bytes(counted, spheres) / max(steps, 1)
+        roof["logical_per_step"] = {"bytes_per_step": int(lg), "ms_per_step": round(ms_pass, 3),
+                                    "achieved": round(lg / (ms_pass / 1e3) / 1e9, 1),
+                                    "def": "cross-check, cache-inclusive (NOT HBM): SURVEY.md 8(d) logical traversal "
+                                           "bytes per pass / ms_per_step; above the HBM peak because traversal reuse "
+                                           "is served by the L1/L2/Infinity Cache"}
+    if pmc and pmc.get("pass_bytes") and steps:
+        ms_pass = elapsed / max(steps, 1) * 1e3
+        roof["frame"] = {"hbm_bytes_per_pass": pmc["pass_bytes"], "ms_per_pass": round(ms_pass, 3),
+                         "achieved": round(pmc["pass_bytes"] / (ms_pass / 1e3) / 1e9, 1),
+                         "frac": round(pmc["pass_bytes"] / (ms_pass / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "def": "measured fabric-side bytes of one pass (every kernel, same PMC run) / timed "
+                                "wall per pass (one GPU's passes overlap 20 at a time)"}
+    iss = load_issue(workload)
+    if iss and steps:
+        ms_pass = elapsed / steps * 1e3
+        v_all, v_tr = iss["per_pass"]["SQ_INSTS_VALU"], iss["trace_per_pass"]["SQ_INSTS_VALU"]
+        rate = v_all / (ms_pass / 1e3) / 1e9
+        roof["valu"] = {"wave_instructions_per_pass": int(v_all), "trace_share": round(v_tr / v_all, 3),
+                        "achieved": round(rate, 1), "peak": VALU_PEAK_GWIS, "unit": "G wave64 VALU instr/s",
+                        "frac": round(rate / VALU_PEAK_GWIS, 4),
+                        "def": "VALU wave-instructions of one pass, every kernel (rocprofv3 --pmc SQ_INSTS_VALU, "
+                               "profiles/pmc_issue.json: %s) / timed wall per pass, against the chip's issue "
+                               "rate (1024 SIMD-32 x 2.4 GHz / 2 cycles)" % iss.get("run", "")}
+    return roof
 
 
 def main():
@@ -235,24 +351,22 @@ def main():
     P = scene.passes
     tile_split = (args.tile_share, 0) if args.tile_share > 1 else (world, rank)
     ren = rtamd.Renderer(scene, sort=sort, device=local, tiles=tile_split + (TILE_ROWS,) if tiles else None)
-    exchange = {"calls": 0, "bytes": 0, "s": 0.0}
+    probe = None
     if tiles and sort and tile_split[0] > 1:
-        # pixel tiles with the reorder on: one byte per global live ray per bounce,
-        # summed over the owners (torch.distributed all_reduce; RCCL's ncclAllReduce in the library's
-        # own multi-GPU path).  The 1-GPU --tile-share probe has no other owners: their slots are
-        # filled as terminated rays, so rank 0's own rays keep a complete (if smaller) global order.
-        def exchange_fn(arr):
-            t0 = time.perf_counter()
-            if use_dist and world > 1:
-                t = torch.from_numpy(arr).to("cuda")
-                dist.all_reduce(t)
-                arr[:] = t.cpu().numpy()
-            else:
-                arr[arr == 0] = 65
-            exchange["calls"] += 1
-            exchange["bytes"] += int(arr.size)
-            exchange["s"] += time.perf_counter() - t0
-        ren.set_exchange(exchange_fn)
+        # pixel tiles with the reorder on: one byte per global live ray per bounce, summed
+        # over the owners on the device.  N > 1 ranks: the renderer joins an RCCL communicator of its
+        # own (rt_renderer_set_exchange_rccl; rank 0's id is broadcast over torch.distributed) and
+        # all-reduces the bytes in place on each pass's stream.  The 1-GPU --tile-share probe has no
+        # other owners: tests/native/xchg.hip emulates their slots on the device (live with the own
+        # rays' live fraction, else terminated), so rank 0 ranks its rays in a global order of a
+        # realistic size; its seeds (and image) are not a real N-GPU run's, so no parity is claimed.
+        if use_dist and world > 1:
+            import rtamd_dist
+            rtamd_dist.join_tile_exchange(dist, ren, rtamd)
+        else:
+            import xchg_lib
+            probe = xchg_lib.EmulatedPeers()
+            probe.attach(ren)
 
     px3 = W * H * 3
     frame = None
@@ -337,7 +451,7 @@ def main():
     elapsed = time.perf_counter() - t0
 
     # ---- untimed legs (every rank takes part: they contain collectives)
-    evrun, counted, frame_s, parity = {}, None, None, None
+    evrun, counted, frame_s, parity, excl = {}, None, None, None, None
     if not args.no_extras:
         # per-launch kernel times: the same steps again with per-bounce HIP events on each pass's stream
         ren.set_event_timing(True)
@@ -376,7 +490,12 @@ def main():
                       if gold else "no golden hash for this workload",
                       "reference_rms": "parity unpinned: the reference's GPU path cannot run here (SURVEY.md §8c), "
                                        "the oracle is a cited restatement; image error vs the reference is not measured"}
+        if not tiles and rank == 0 and not args.no_counters:
+            excl = exclusive_pass(scene, sort, local)
     elapsed, frame_s_max = reduce([elapsed, frame_s or 0.0], "max")
+    # ranks that took part, as the collective backend counts them (a SCALE run can be checked for
+    # RCCL seeing N ranks): an all-reduce of 1 per rank
+    n_ranks_seen = int(reduce([1.0])[0])
     live, gen = reduce([timed.get("live_segments", 0), timed.get("generated_rays", 0)])
 
     if rank == 0:
@@ -386,52 +505,8 @@ def main():
         launches = int(evrun.get("trace_launches", 0))
         trace_ms = evrun.get("trace_ms", 0.0) / launches if launches else 0.0
         roof = None
-        if counted and launches and trace_ms > 0:
-            # this rank's counted launches (the same steps as the event re-run)
-            comp = compulsory_trace_bytes(counted, scene_bytes, launches) / launches
-            logical = logical_trace_bytes(counted, v.sphere_count) / launches
-            achieved = comp / (trace_ms / 1e3) / 1e9
-            pmc = load_pmc(workload)
-            traffic = pmc["trace_bytes_per_launch"] if pmc else None
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "trace_kernel (BVH traversal + Moller-Trumbore + slab + sphere loop), per launch",
-                    "bytes_per_launch": int(comp), "ms_per_launch": round(trace_ms, 4), "launches": launches,
-                    "achieved_def": "algorithmic HBM bytes per trace launch (24 B ray read per live segment past "
-                                    "bounce 0 + 8 B hit write per live segment + the scene's node/triangle arrays "
-                                    "once, reference layouts) / average trace launch duration (device wall clock from "
-                                    "the launch's first wave start to its last wave end, read in an untimed re-run of "
-                                    "the timed steps; up to 20 passes share the chip, so a launch's duration includes "
-                                    "time it shared, as in rocprofv3's kernel trace)",
-                    "traffic_def": None if not pmc else
-                    "measured HBM-side bytes per trace launch, rocprofv3 --pmc, one profiled pass "
-                    "(%s; reads priced by request size TCC_EA0_RDREQ_{128B,64B,32B}, = 2 x FETCH_SIZE for 128-B "
-                    "requests per MI355X_MICROARCH.md §HBM; writes TCC_EA0_WRREQ{,_64B}); %s" % (pmc["file"], pmc.get("run", "")),
-                    "traffic_frac": round(traffic / (trace_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
-                    "l2": {"achieved": round(logical / (trace_ms / 1e3) / 1e9, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(logical / (trace_ms / 1e3) / 1e9 / L2_PEAK_GBS, 4),
-                           "bytes_per_launch": int(logical),
-                           "def": "SURVEY.md 8(d) logical cache-inclusive bytes of the traversal (24 B ray + 16 B x S "
-                                  "+ 32 B x node pops + 64 B x internal visits + 48 B x triangle tests + 8 B hit) per "
-                                  "launch / launch duration, against the aggregate L2 rate (MI355X_MICROARCH.md §L2)"}}
-            if pmc and pmc.get("pass_bytes"):
-                ms_pass = elapsed / max(steps, 1) * 1e3
-                roof["frame"] = {"hbm_bytes_per_pass": pmc["pass_bytes"], "ms_per_pass": round(ms_pass, 3),
-                                 "achieved": round(pmc["pass_bytes"] / (ms_pass / 1e3) / 1e9, 1),
-                                 "frac": round(pmc["pass_bytes"] / (ms_pass / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                                 "def": "measured HBM-side bytes of one pass (every kernel, same PMC run) / timed "
-                                        "wall per pass (one GPU's passes overlap 20 at a time)"}
-            iss = load_issue(workload)
-            if iss and steps:
-                ms_pass = elapsed / steps * 1e3
-                v_all, v_tr = iss["per_pass"]["SQ_INSTS_VALU"], iss["trace_per_pass"]["SQ_INSTS_VALU"]
-                rate = v_all / (ms_pass / 1e3) / 1e9
-                roof["valu"] = {"wave_instructions_per_pass": int(v_all), "trace_share": round(v_tr / v_all, 3),
-                                "achieved": round(rate, 1), "peak": VALU_PEAK_GWIS, "unit": "G wave64 VALU instr/s",
-                                "frac": round(rate / VALU_PEAK_GWIS, 4),
-                                "def": "VALU wave-instructions of one pass, every kernel (rocprofv3 --pmc SQ_INSTS_VALU, "
-                                       "profiles/pmc_issue.json: %s) / timed wall per pass, against the chip's issue "
-                                       "rate (1024 SIMD-32 x 2.4 GHz / 2 cycles)" % iss.get("run", "")}
+        if counted and launches and trace_ms > 0 and excl:
+            roof = roofline(excl, counted, launches, trace_ms, scene_bytes, v.sphere_count, workload, elapsed, steps)
         value = live / elapsed / 1e6 if elapsed > 0 else 0.0
         nominal = gen * bounces / elapsed / 1e6 if elapsed > 0 else 0.0
         ms_step = elapsed / steps * 1e3 if steps else 0.0
@@ -465,6 +540,7 @@ def main():
                                                                   ("; its rounds of full 20-spp passes of the extended "
                                                                    "frame" if frame_spp != spp else "")),
                 "passes_per_frame": P,
+                "n_ranks_seen": n_ranks_seen,
                 **({"frame_extended": "%d spp (%d passes) instead of %d, so that each of the %d GPUs renders its %d "
                                       "passes in one batch" % (frame_spp, P, spp, world, steps)}
                    if frame_spp != spp else {}),
@@ -474,13 +550,11 @@ def main():
                 "scene_load_s": round(load_s, 3),
                 "bvh_ms": round(scene.bvh_ms, 1),
                 **({"tile_share_probe": "rank 0's %d-row stripes of a %d-GPU split, on one GPU"
-                    % (TILE_ROWS, args.tile_share) + (" (sort on: the other owners' bucket bytes are filled as "
-                                                      "terminated rays)" if sort else "")} if args.tile_share > 1 else {}),
-                **({"tile_exchange": {"calls": exchange["calls"], "bytes": exchange["bytes"],
-                                      "host_s": round(exchange["s"], 4),
-                                      "def": "per-bounce bucket-byte exchanges of every run of this process (timed, "
-                                             "event, counter and frame legs), host time inside the exchange"}}
-                   if exchange["calls"] else {}),
+                    % (TILE_ROWS, args.tile_share) + (" (sort on: the other owners' global slots emulated on the "
+                                                      "device by tests/native/xchg.hip, live with the own rays' "
+                                                      "live fraction else terminated; an approximation of the "
+                                                      "N-GPU share's work, not its image)" if sort else "")}
+                   if args.tile_share > 1 else {}),
             },
             "parity": parity,
             "roofline": roof,
@@ -496,6 +570,8 @@ def main():
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), file=json_out, flush=True)
     ren.close()
+    if probe:
+        probe.close()
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()

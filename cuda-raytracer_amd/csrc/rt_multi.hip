@@ -36,6 +36,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -45,6 +46,7 @@
 namespace rtamd {
 int fail(int code, const std::string &msg);
 }
+extern "C" int rtamd_renderer_set_poll(rt_renderer *r, int (*fn)(void *), void *user);   // rt_render.hip
 extern "C" int rtamd_renderer_run_pitched(rt_renderer *r, int pass_begin, int count, int stride,
                                           float *d_pass_sums, size_t pitch, rt_stats *stats);   // rt_render.hip
 
@@ -76,32 +78,50 @@ struct DevState {
 // A device that fails must not leave its peers blocked in a collective.  Every device first builds
 // its renderer and buffers (where nearly every failure happens: out of memory, a bad scene) and
 // meets the others; if any failed, all return before the first collective.  A failure after that
-// aborts every communicator, which ends the peers' pending collectives with an error.
+// sets `failed`; every device aborts only its OWN communicator (its thread is the only one that
+// uses it, so no call can race the abort), when it fails itself or when it sees the flag: before
+// each RCCL call and while it polls a stream or event that waits on a collective.  The aborted
+// communicator's pending kernels end, and its peers' polls see the flag and abort theirs.
 struct Sync {
     std::mutex m;
     std::condition_variable cv;
     int world = 0, arrived = 0;
-    bool failed = false;
-    std::vector<ncclComm_t> *comms = nullptr;
-    std::atomic<bool> aborted{false};
+    bool setup_failed = false;
+    std::atomic<bool> failed{false};
     bool setup_done(bool ok) {   // false if any device's setup failed
         std::unique_lock<std::mutex> l(m);
-        if (!ok) failed = true;
+        if (!ok) setup_failed = true;
         if (++arrived == world) cv.notify_all();
         else cv.wait(l, [&] { return arrived == world; });
-        return !failed;
-    }
-    void abort() {
-        bool expected = false;
-        if (aborted.compare_exchange_strong(expected, true))
-            for (ncclComm_t c : *comms) (void)ncclCommAbort(c);
+        return !setup_failed;
     }
 };
 
+// One device's communicator and its abort state (touched by that device's thread only).
+struct Link {
+    ncclComm_t comm = nullptr;
+    bool aborted = false;
+    Sync *sy = nullptr;
+    void abort() {
+        if (!aborted && comm) (void)ncclCommAbort(comm);
+        aborted = true;
+    }
+    // nonzero (and the communicator aborted) once any device has failed
+    int check() {
+        if (!sy->failed.load()) return 0;
+        abort();
+        return RT_E_INVALID;
+    }
+};
+
+// the renderer's abort poll (rtamd_renderer_set_poll): a tile exchange waits on this device's collective
+int link_poll(void *user) { return static_cast<Link *>(user)->check(); }
+
 // Scope guard of one device's run: arrives at the setup barrier as failed if the run ends before
-// setup(), and aborts the communicators if it ends with an error after it.
+// setup(), and on an error after it raises the flag and aborts this device's communicator.
 struct RunGuard {
     Sync &sy;
+    Link &ln;
     bool arrived = false, ok = false;
     bool setup() {
         arrived = true;
@@ -109,7 +129,10 @@ struct RunGuard {
     }
     ~RunGuard() {
         if (!arrived) (void)sy.setup_done(false);
-        else if (!ok) sy.abort();
+        else if (!ok) {
+            sy.failed = true;
+            ln.abort();
+        }
     }
 };
 
@@ -127,16 +150,41 @@ int hip_err(hipError_t e, const char *what) {
     } while (0)
 #define MNCCL(call)                                                                                       \
     do {                                                                                                  \
+        if (ln.check()) return rtamd::fail(RT_E_INVALID, "another device of the render failed");         \
         const ncclResult_t r_ = (call);                                                                   \
         if (r_ != ncclSuccess) return rtamd::fail(RT_E_HIP, std::string("Error ") + #call + " " + nccl_str(r_)); \
     } while (0)
 
 namespace {
 
+// Test hook: RTAMD_FAIL_AFTER_SETUP=<rank> makes that device fail right after the setup barrier, the
+// path where its peers must not be left inside a collective.
+bool injected_failure(int rank) {
+    const char *e = std::getenv("RTAMD_FAIL_AFTER_SETUP");
+    return e && *e && std::atoi(e) == rank;
+}
+
+// Waits for stream s (which holds collectives) while watching the other devices: returns an error
+// (and aborts this device's communicator) if one of them failed.
+int wait_stream(hipStream_t s, Link &ln) {
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) return RT_OK;
+        if (q != hipErrorNotReady) return hip_err(q, "hipStreamQuery");
+        if (ln.check()) return rtamd::fail(RT_E_INVALID, "another device of the render failed");
+        std::this_thread::yield();
+    }
+}
+#define MWAIT(s)                                   \
+    do {                                           \
+        if (int rc_ = wait_stream((s), ln)) return rc_; \
+    } while (0)
+
 // Device `st.rank`'s share of the frame: render, exchange, add; the root also gathers.
-int run_device(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int world, DevState &st,
-               float *fb_out, Sync &sy) {
-    RunGuard run{sy};
+int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, DevState &st, float *fb_out,
+               Sync &sy) {
+    RunGuard run{sy, ln};
+    ncclComm_t comm = ln.comm;
     MHIP(hipSetDevice(st.device));
     const int P = (scene->ray_count + 19) / 20;
     const size_t px3 = (size_t)scene->width * scene->height * 3;
@@ -176,6 +224,7 @@ int run_device(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int 
     MHIP(hipMemsetAsync(slice, 0, sl * sizeof(float), g.s));
     MHIP(hipStreamSynchronize(g.s));
     if (!run.setup()) return rtamd::fail(RT_E_INVALID, "another device of the render failed");
+    if (injected_failure(st.rank)) return rtamd::fail(RT_E_INVALID, "injected failure (RTAMD_FAIL_AFTER_SETUP)");
     using clk = std::chrono::high_resolution_clock;
     for (int k0 = 0; k0 < R; k0 += chunk) {
         const int m = std::min(chunk, R - k0);
@@ -215,14 +264,14 @@ int run_device(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int 
                            world, m, k0, P);
         MHIP(hipGetLastError());
         // the next chunk's render overwrites buf: the exchange must have read it
-        MHIP(hipStreamSynchronize(g.s));
+        MWAIT(g.s);
         st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     }
     const auto t0 = clk::now();
     // gather the finished slices to the root (in place: the root's own slice is block 0)
     MNCCL(ncclGather(slice, slice, sl, ncclFloat32, 0, comm, g.s));
     if (st.rank == 0) MHIP(hipMemcpyAsync(fb_out, slice, px3 * sizeof(float), hipMemcpyDeviceToHost, g.s));
-    MHIP(hipStreamSynchronize(g.s));
+    MWAIT(g.s);
     st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     run.ok = true;
     return RT_OK;
@@ -230,18 +279,21 @@ int run_device(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int 
 
 // Pixel tiles with the reorder on: the per-bounce bucket bytes summed over the devices in place
 // (ncclAllReduce, uint8: every global slot has one owner, no byte exceeds 65), on the pass's stream.
+// An aborted run (another device failed) issues no further collective.
 int nccl_exchange(void *user, uint8_t *bytes, uint64_t n, void *stream) {
-    const ncclResult_t r = ncclAllReduce(bytes, bytes, n, ncclUint8, ncclSum, *static_cast<ncclComm_t *>(user),
-                                         static_cast<hipStream_t>(stream));
+    Link &ln = *static_cast<Link *>(user);
+    if (ln.check()) return RT_E_INVALID;
+    const ncclResult_t r = ncclAllReduce(bytes, bytes, n, ncclUint8, ncclSum, ln.comm, static_cast<hipStream_t>(stream));
     return r == ncclSuccess ? 0 : -(int)r - 1;
 }
 
 // Device `st.rank`'s tiles: owner rank's tile_rows-row stripes of every pass, then an
 // ncclReduce of the owners' framebuffers to the root: every pixel has one owner and is 0 elsewhere,
 // so the sum is that owner's value bit for bit (x + 0 = x).
-int run_device_tiles(const rt_scene *scene, const rt_opts *base, ncclComm_t comm, int world, DevState &st,
+int run_device_tiles(const rt_scene *scene, const rt_opts *base, Link &ln, int world, DevState &st,
                      float *fb_out, Sync &sy) {
-    RunGuard run{sy};
+    RunGuard run{sy, ln};
+    ncclComm_t comm = ln.comm;
     MHIP(hipSetDevice(st.device));
     const size_t px3 = (size_t)scene->width * scene->height * 3;
     rt_opts o = *base;
@@ -268,12 +320,15 @@ int run_device_tiles(const rt_scene *scene, const rt_opts *base, ncclComm_t comm
         }
     } g{ren};
     if (o.sort && world > 1) {
-        rc = rt_renderer_set_exchange(ren, nccl_exchange, &comm, 1);
+        rc = rt_renderer_set_exchange(ren, nccl_exchange, &ln, 1);
+        if (rc) return rc;
+        rc = rtamd_renderer_set_poll(ren, link_poll, &ln);
         if (rc) return rc;
     }
     MHIP(hipMalloc(reinterpret_cast<void **>(&g.d), px3 * sizeof(float)));
     MHIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
     if (!run.setup()) return rtamd::fail(RT_E_INVALID, "another device of the render failed");
+    if (injected_failure(st.rank)) return rtamd::fail(RT_E_INVALID, "injected failure (RTAMD_FAIL_AFTER_SETUP)");
     rt_stats s{};
     using clk = std::chrono::high_resolution_clock;
     rc = rtamd_renderer_run_pitched(ren, 0, -1, 1, nullptr, 0, &s);
@@ -284,7 +339,7 @@ int run_device_tiles(const rt_scene *scene, const rt_opts *base, ncclComm_t comm
     const auto t0 = clk::now();
     MNCCL(ncclReduce(g.d, g.d, px3, ncclFloat32, ncclSum, 0, comm, g.s));
     if (st.rank == 0) MHIP(hipMemcpyAsync(fb_out, g.d, px3 * sizeof(float), hipMemcpyDeviceToHost, g.s));
-    MHIP(hipStreamSynchronize(g.s));
+    MWAIT(g.s);
     st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     run.ok = true;
     return RT_OK;
@@ -311,24 +366,31 @@ int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out
         opts->pass_stride > 1)
         return rtamd::fail(RT_E_INVALID, "multi-device rt_render renders the whole frame (pass_begin 0, all passes)");
     std::vector<ncclComm_t> comms(world);
-    MNCCL(ncclCommInitAll(comms.data(), world, devs.data()));
+    {
+        const ncclResult_t r = ncclCommInitAll(comms.data(), world, devs.data());
+        if (r != ncclSuccess) return rtamd::fail(RT_E_HIP, std::string("Error ncclCommInitAll ") + nccl_str(r));
+    }
     std::vector<DevState> st(world);
     Sync sy;
     sy.world = world;
-    sy.comms = &comms;
+    std::vector<Link> links(world);
+    for (int k = 0; k < world; k++) {
+        links[k].comm = comms[k];
+        links[k].sy = &sy;
+    }
     std::vector<std::thread> th;
     for (int k = 0; k < world; k++) {
         st[k].device = devs[k];
         st[k].rank = k;
         th.emplace_back([&, k]() {
-            st[k].rc = opts->shard_tiles ? run_device_tiles(scene, opts, comms[k], world, st[k], fb_out, sy)
-                                         : run_device(scene, opts, comms[k], world, st[k], fb_out, sy);
+            st[k].rc = opts->shard_tiles ? run_device_tiles(scene, opts, links[k], world, st[k], fb_out, sy)
+                                         : run_device(scene, opts, links[k], world, st[k], fb_out, sy);
             if (st[k].rc) st[k].err = rt_last_error();
         });
     }
     for (auto &t : th) t.join();
-    if (!sy.aborted)    // ncclCommAbort already freed them
-        for (auto c : comms) (void)ncclCommDestroy(c);
+    for (auto &l : links)
+        if (!l.aborted) (void)ncclCommDestroy(l.comm);   // ncclCommAbort already freed the others
     // report the device that failed first-hand, not a peer that returned because of it
     for (auto &s : st)
         if (s.rc && s.err.find("another device") == std::string::npos) return rtamd::fail(s.rc, s.err);

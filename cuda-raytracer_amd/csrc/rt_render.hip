@@ -23,7 +23,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <rccl/rccl.h>
 
 #pragma clang fp contract(off)
 
@@ -224,6 +227,35 @@ __device__ __forceinline__ void slab_pair(float4 a, float4 b, float4 c, V3 o, fl
     h1 = n1 <= f1;
 }
 
+// Möller–Trumbore (scene.cu:160-195, rt_device.h ray_triangle) with the early-outs folded into one
+// predicate: every quantity is computed for every lane and the accept test is the conjunction of
+// the reference's four reject tests, negated exactly as written (a NaN u, v or t rejects nothing,
+// as in the branchy form).  Same values, same outcome; no divergent exec-mask regions.
+#ifndef RT_MT_FLAT
+#define RT_MT_FLAT 0
+#endif
+#ifndef RT_POP_FLAT
+#define RT_POP_FLAT 0
+#endif
+#ifndef RT_DESC_FLAT
+#define RT_DESC_FLAT 0
+#endif
+__device__ __forceinline__ bool ray_triangle_flat(V3 o, V3 d, V3 p1, V3 e1, V3 e2, float closest, float &t) {
+    const V3 h = cross(d, e2);
+    const float a = dot(h, e1);
+    const float f = 1 / a;
+    const V3 s = o - p1;
+    const float u = dot(s, h) * f;
+    const V3 q = cross(s, e1);
+    const float v = dot(d, q) * f;
+    t = dot(e2, q) * f;
+    const bool ok_a = a != 0;
+    const bool ok_u = !(u < 0 || u > 1);
+    const bool ok_v = !(v < 0 || u + v > 1);
+    const bool ok_t = !(t < kEps || t >= closest);
+    return ok_a & ok_u & ok_v & ok_t;
+}
+
 // Triangle range [ti, te) of a leaf ref (small leaves inline, big ones through big_leaves).
 __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int &ti, int &te) {
     if (ref & kBigLeaf) {
@@ -402,7 +434,13 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             const float q2 = c.x;
             if (COUNT) tt++;
             float t;
-            if (ray_triangle(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t)) {
+            const bool hit = RT_MT_FLAT
+                ? ray_triangle_flat(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t)
+                : ray_triangle(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t);
+            if (RT_MT_FLAT) {
+                closest = hit ? t : closest;
+                index = hit ? S.sphere_count + ti : index;
+            } else if (hit) {
                 closest = t;
                 index = S.sphere_count + ti;
             }
@@ -441,6 +479,18 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             if (both) sp++;
             ref = any ? next_ref : ref;
             const bool descend = any && !(next_t >= closest);
+#if RT_DESC_FLAT
+            // entering the next node as selects; only a big leaf's range takes a (rare) branch
+            if (COUNT) pn += descend ? 1u : 0u;
+            const bool leaf = descend && (ref & kLeaf);
+            if (__builtin_expect(leaf && (ref & kBigLeaf), 0)) {
+                leaf_range(S, ref, ti, te);
+            } else {
+                ti = leaf ? (int)(ref & 0xFFFFFFu) : ti;
+                te = leaf ? ti + (int)((ref >> 24) & 0x3Fu) : te;
+            }
+            need = !descend || (leaf && ti == te);
+#else
             need = !descend;
             if (descend) {
                 if (COUNT) pn++;
@@ -449,10 +499,43 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     need = ti == te;
                 }
             }
+#endif
         }
 #ifdef RT_PROFILE
         if (__ballot(need)) PROF(5, 1);
 #endif
+#if RT_POP_FLAT
+        // The same pops as below with the per-entry decisions as selects: the LDS entry is read for
+        // every popping lane (an empty stack reads entry 0, unused), only the rare overflow-stack
+        // entries and big-leaf ranges take a branch.
+        while (need) {
+            PROF(10, 1);
+            const bool empty = sp == 0;
+            sp = empty ? 0 : sp - 1;
+            uint2 e = col[min(sp, kStackLds) * kBlock];
+            // opaque: keeps the LDS read an LDS read (the compiler would otherwise fold it and the
+            // rare overflow read below into one flat load through a selected pointer)
+            asm volatile("" : "+v"(e.x), "+v"(e.y));
+            if (__builtin_expect(__ballot(sp >= kStackLds) != 0, 0)) {   // wave-uniform, rare
+                if (sp >= kStackLds) {
+                    e.x = overflow[(sp - kStackLds) * lanes + gl];
+                    e.y = overflow[dist_half + (sp - kStackLds) * lanes + gl];
+                }
+            }
+            const bool take = !empty && !(__uint_as_float(e.y) >= closest);
+            slot = empty ? -2 - slot : slot;   // done; {closest, index} stored at the next refill or at exit
+            ref = take ? e.x : ref;
+            if (COUNT) pn += take ? 1u : 0u;
+            const bool leaf = take && (ref & kLeaf);
+            if (__builtin_expect(leaf && (ref & kBigLeaf), 0)) {
+                leaf_range(S, ref, ti, te);
+            } else {
+                ti = leaf ? (int)(ref & 0xFFFFFFu) : ti;
+                te = leaf ? ti + (int)((ref >> 24) & 0x3Fu) : te;
+            }
+            need = !empty && (!take || (leaf && ti == te));
+        }
+#else
         while (need) {                  // pop to the next entry nearer than closest
             PROF(10, 1);
             if (sp == 0) {
@@ -479,6 +562,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 need = ti == te;
             }
         }
+#endif
     }
     if (slot <= -2) hits[-2 - slot] = make_float2(closest, __int_as_float(index));
     Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
@@ -815,37 +899,70 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
 
 // ---- pixel tiles with the reorder on: the global bucket array and the global rank
 // Every live ray of this owner writes bucket + 1 at its global slot (bounce 0: its ray index) of
-// the zeroed array G; the exchange sums G over the owners.
-__global__ __launch_bounds__(kBlock) void zero_bytes_kernel(uint8_t *__restrict__ g, const uint32_t *__restrict__ count) {
+// two zeroed arrays: G, which the exchange sums over the owners, and L, this owner's own bytes
+// (L[g] != 0 iff this owner holds global slot g), which the global ranking uses to write new
+// positions only for this owner's slots.
+__global__ __launch_bounds__(kBlock) void zero_bytes_kernel(uint8_t *__restrict__ g, uint8_t *__restrict__ l,
+                                                            const uint32_t *__restrict__ count) {
     const uint32_t n = *count;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) g[i] = 0;
+    const uint32_t n16 = n / 16;        // 16-B stores for the bulk (buffers are hipMalloc-aligned)
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n16; i += gridDim.x * kBlock) {
+        reinterpret_cast<uint4 *>(g)[i] = make_uint4(0, 0, 0, 0);
+        reinterpret_cast<uint4 *>(l)[i] = make_uint4(0, 0, 0, 0);
+    }
+    for (uint32_t i = n16 * 16 + blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) g[i] = l[i] = 0;
 }
 template <int FIRST>
 __global__ __launch_bounds__(kBlock) void tile_bytes_kernel(const uint8_t *__restrict__ bkt, const uint32_t *__restrict__ live_count,
                                                             const uint32_t *__restrict__ gslot, SlotMap map,
-                                                            uint8_t *__restrict__ g) {
+                                                            uint8_t *__restrict__ g, uint8_t *__restrict__ l) {
     const uint32_t n = *live_count;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
-        g[FIRST ? map.ray(i) : gslot[i]] = (uint8_t)(bkt[i] + 1);
-}
-// After the exchange: G holds bucket + 1 for every global live slot; back to buckets in place.  A
-// byte outside [1, 65] (a slot no owner wrote, or an exchange that did not sum) is counted in
-// *bad and made a terminated ray, so no bucket index ever leaves [0, 64]; the host fails the render.
-__global__ __launch_bounds__(kBlock) void unbias_bytes_kernel(uint8_t *__restrict__ g, const uint32_t *__restrict__ count,
-                                                              uint32_t *__restrict__ bad) {
-    const uint32_t n = *count;
-    uint32_t nbad = 0;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const uint32_t v = g[i];
-        const bool ok = v >= 1 && v <= kBuckets;
-        nbad += ok ? 0u : 1u;
-        g[i] = (uint8_t)(ok ? v - 1 : kDead);
+        const uint32_t s = FIRST ? map.ray(i) : gslot[i];
+        const uint8_t v = (uint8_t)(bkt[i] + 1);
+        g[s] = v;
+        l[s] = v;
     }
-    if (nbad) atomicAdd(bad, nbad);
 }
-// The stable sort's new position of every live global slot (the scatter's ranking without the
-// move): newpos[g] = slots of smaller buckets + earlier slots of the same bucket.
-__global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__restrict__ bkt_in,
+// After the exchange G holds bucket + 1 for every global live slot.  A byte outside [1, 65] (a slot
+// no owner wrote, or an exchange that did not sum) is counted in *bad and read as a terminated ray,
+// so no bucket index ever leaves [0, 64]; the host fails the render.
+__device__ __forceinline__ uint32_t exchanged_bucket(uint32_t v) { return (v >= 1 && v <= kBuckets) ? v - 1 : kDead; }
+
+// Per-tile bucket counts of the exchanged global array (sort_hist_kernel on biased bytes).
+__global__ __launch_bounds__(kBlock) void gsort_hist_kernel(const uint8_t *__restrict__ g,
+                                                            const uint32_t *__restrict__ live_count, int tiles,
+                                                            uint32_t *__restrict__ counts, uint32_t *__restrict__ bad) {
+    const int n = (int)*live_count;
+    __shared__ uint32_t h[kBuckets];
+    uint32_t nbad = 0;
+    for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {
+        for (int b = threadIdx.x; b < kBuckets; b += kBlock) h[b] = 0;
+        __syncthreads();
+        const int base = tile * kSortTile;
+#pragma unroll 4
+        for (int r = 0; r < kSortItems; r++) {
+            if (base + r * kBlock >= n) break;
+            const int item = base + r * kBlock + threadIdx.x;
+            const bool valid = item < n;
+            const uint32_t v = valid ? g[item] : 1u;
+            const uint32_t b = exchanged_bucket(v);
+            nbad += (valid && !(v >= 1 && v <= kBuckets)) ? 1u : 0u;
+            const unsigned long long peers = match_bucket(b, valid);
+            if (valid && rank_below(peers) == 0) atomicAdd(&h[b], (uint32_t)__popcll(peers));
+        }
+        __syncthreads();
+        for (int b = threadIdx.x; b < kBuckets; b += kBlock) counts[(size_t)b * tiles + tile] = h[b];
+        __syncthreads();
+    }
+    const unsigned long long s = wave_sum(nbad);
+    if (lane_id() == 0 && s) atomicAdd(bad, (uint32_t)s);
+}
+// The stable sort's new position of this owner's live global slots (the scatter's ranking without
+// the move): newpos[g] = slots of smaller buckets + earlier slots of the same bucket, written only
+// where own[g] != 0 (the other owners' slots are ranked, not stored).
+__global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__restrict__ g_in,
+                                                           const uint8_t *__restrict__ own,
                                                            const uint32_t *__restrict__ live_count, int tiles,
                                                            const uint32_t *__restrict__ offsets,
                                                            const uint32_t *__restrict__ totals,
@@ -863,12 +980,13 @@ __global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__rest
         for (int r = 0; r < rounds; r++) {
             const int item = base + r * kBlock + threadIdx.x;
             const bool valid = item < n;
-            const uint32_t b = valid ? bkt_in[item] : 0u;
+            const uint32_t b = valid ? exchanged_bucket(g_in[item]) : 0u;
+            const bool mine = valid && own[item] != 0;
             const unsigned long long peers = match_bucket(b, valid);
             const uint32_t rank = rank_below(peers);
             if (valid && rank == 0) wcount[wave][b] = (uint32_t)__popcll(peers);
             __syncthreads();
-            if (valid && b != kDead) {
+            if (mine && b != kDead) {
                 uint32_t pos = run[b] + rank;
                 for (int k = 0; k < wave; k++) pos += wcount[k][b];
                 newpos[item] = pos;
@@ -1090,12 +1208,15 @@ struct PassCtx {
     DevBuf<float2> hits;
     DevBuf<float> psum;               // this pass's per-pixel sums (when the caller gives no buffer)
     // pixel tiles with the reorder on: global slot per ray (ping-pong with the state), the global
-    // bucket bytes, their ranks, the global live count {current, next} and its host copy
+    // bucket bytes (exchanged) and this owner's own bytes, their ranks, the global live count
+    // {current, next, bad bytes of the run} and its host copy (pinned; lg_ready is recorded after
+    // the copy, so the host waits for the count, not for the bounce queued behind it)
     DevBuf<uint32_t> gslot[2], newpos, glive;
-    DevBuf<uint8_t> gbytes;
-    uint32_t *lg_host = nullptr;      // pinned
+    DevBuf<uint8_t> gbytes, lbytes;
+    uint32_t *lg_host = nullptr;
+    hipEvent_t lg_ready = nullptr;
     // state of this context's pass in the tiled sort-on schedule
-    int t_p = 0, t_rtc = 0, t_rem = 0, t_n = 0, t_cur = 0, t_tiles_g = 0;
+    int t_p = 0, t_k = 0, t_b = -1, t_rtc = 0, t_rem = 0, t_n = 0, t_cur = 0, t_tiles_g = 0;
     uint64_t t_lg = 0;
     hipEvent_t fb_done = nullptr;     // recorded after this context last added into the framebuffer
     hipEvent_t done = nullptr;
@@ -1104,6 +1225,7 @@ struct PassCtx {
 
     ~PassCtx() {
         if (lg_host) (void)hipHostFree(lg_host);
+        if (lg_ready) (void)hipEventDestroy(lg_ready);
         for (auto e : events) (void)hipEventDestroy(e);
         if (fb_done) (void)hipEventDestroy(fb_done);
         if (done) (void)hipEventDestroy(done);
@@ -1163,6 +1285,12 @@ struct rt_renderer {
     hipEvent_t t_begin = nullptr, t_end = nullptr;
 
     ~rt_renderer() {
+        if (xcomm) {
+            (void)hipSetDevice(device);
+            for (auto &c : ctx)
+                if (c.stream) (void)hipStreamSynchronize(c.stream);
+            (void)ncclCommDestroy(static_cast<ncclComm_t>(xcomm));
+        }
         if (xhost) (void)hipHostFree(xhost);
         if (t_begin) (void)hipEventDestroy(t_begin);
         if (t_end) (void)hipEventDestroy(t_end);
@@ -1174,6 +1302,12 @@ struct rt_renderer {
     void *xuser = nullptr;
     bool x_on_device = false;
     uint8_t *xhost = nullptr;         // pinned staging of a host exchange
+    // abort check polled while the host waits for a count behind an exchange (rt_multi: a peer
+    // device that failed never sends its bytes); nonzero = give up with that error code
+    int (*xpoll)(void *) = nullptr;
+    void *xpoll_user = nullptr;
+    // RCCL communicator owned by this renderer (rt_renderer_set_exchange_rccl), or null
+    void *xcomm = nullptr;
     bool tsort() const { return tile_count > 1 && sort; }
     int pass_count() const { return (spp + 19) / 20; }
     bool tiled() const { return tile_count > 1; }
@@ -1310,7 +1444,7 @@ struct rt_renderer {
         const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
         // than half of the free device memory holds (1080p: ~2.9 GB per context).
-        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8) +
+        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0)) +
                                  (size_t)trace_blocks_max * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
         size_t mem_free = 0, mem_total = 0;
         HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
@@ -1343,10 +1477,12 @@ struct rt_renderer {
             if (tsort()) {
                 for (int q = 0; q < 2; q++)
                     if ((rc = c.gslot[q].alloc((size_t)max_rays))) return rc;
+                // global arrays: every live slot of the whole image (max_rays = W*H*min(spp, 20))
                 if ((rc = c.newpos.alloc((size_t)max_rays)) || (rc = c.gbytes.alloc((size_t)max_rays)) ||
-                    (rc = c.glive.alloc(3)))
+                    (rc = c.lbytes.alloc((size_t)max_rays)) || (rc = c.glive.alloc(3)))
                     return rc;
                 HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c.lg_host), sizeof(uint32_t)));
+                HIPCHK(hipEventCreateWithFlags(&c.lg_ready, hipEventDisableTiming));
             }
         }
         tm.mark("pass contexts");
@@ -1520,13 +1656,35 @@ struct rt_renderer {
     }
 
     // ---- pixel tiles with the reorder on (rt_renderer_set_exchange)
-    // A group of passes in flight advances bounce by bounce in lockstep: every pass's trace and shade
-    // (+ its bucket bytes) are enqueued, then pass by pass the bytes are exchanged (one host sync per
-    // pass and bounce: the all-reduce count is the global live count) and the global ranking and the
-    // local reorder are enqueued.  Every owner issues its exchanges in the same order.
-    int tsort_begin(PassCtx &c, int p) {
+    // The passes in flight advance in steps: every step, each active context enqueues one bounce's
+    // trace and shade (+ its bucket bytes), then context by context the bytes are exchanged and the
+    // global ranking and the local reorder are enqueued.  The exchange of bounce b needs the global
+    // live count Lg_b on the host (the all-reduce's element count); it was copied to pinned memory at
+    // the end of bounce b - 1, so the host waits for that copy's event, never for the trace and
+    // shade of bounce b queued behind it, and every stream keeps a bounce of work queued while the
+    // host waits.  A context that finishes its pass starts the next one at the next step, and the
+    // contexts' first passes start at staggered steps, so heavy first bounces and latency-bound tail
+    // bounces of different passes overlap as in the untiled pipeline.  The schedule depends only on
+    // the pass count, so every owner issues its exchanges in the same order (what one RCCL
+    // communicator needs).
+    int wait_event(hipEvent_t e) {
+        if (!xpoll) {
+            HIPCHK(hipEventSynchronize(e));
+            return RT_OK;
+        }
+        for (;;) {      // abortable wait (multi-device renders: a failed peer never sends its bytes)
+            const hipError_t q = hipEventQuery(e);
+            if (q == hipSuccess) return RT_OK;
+            if (q != hipErrorNotReady) return hip_fail(q, "hipEventQuery");
+            if (int rc = xpoll(xpoll_user)) return rtamd::fail(rc, "tile exchange aborted: another device of the render failed");
+            std::this_thread::yield();
+        }
+    }
+    int tsort_begin(PassCtx &c, int p, int k) {
         const int before = spp - 20 * p;
         c.t_p = p;
+        c.t_k = k;
+        c.t_b = 0;
         c.t_rtc = std::min(before, 20);
         c.t_rem = before - c.t_rtc;
         c.t_n = (int)(c.t_rtc * tile_pixels());
@@ -1536,7 +1694,6 @@ struct rt_renderer {
         hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, c.stream, c.live.p, (uint32_t)c.t_n, bounces + 1,
                            c.queue.p, nullptr);
         hipLaunchKernelGGL(set_count_kernel, dim3(1), dim3(64), 0, c.stream, c.glive.p, (uint32_t)c.t_lg, nullptr);
-        HIPCHK(hipMemsetAsync(c.glive.p + 2, 0, sizeof(uint32_t), c.stream));
         HIPCHK(hipGetLastError());
         return RT_OK;
     }
@@ -1557,8 +1714,14 @@ struct rt_renderer {
         uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
         const int last = b + 1 == bounces;
         const int cur = c.t_cur;
+        if (!last) {
+            // zero G and L over the global live prefix, even for an owner without rays: its zeros are
+            // its part of the sum (an owner with no stripe, e.g. more owners than stripes)
+            const int zgrid = std::max(1, std::min(blocks_for((int64_t)(c.t_lg + 15) / 16), cus * 8));
+            hipLaunchKernelGGL(zero_bytes_kernel, dim3(zgrid), dim3(kBlock), 0, st, c.gbytes.p, c.lbytes.p, c.glive.p);
+        }
         if (c.t_n == 0) return RT_OK;
-#define RT_TS(COUNT)                                                                                               \
+#define RT_TS(COUNT)                                                                                           \
     do {                                                                                                           \
         if (b == 0) {                                                                                              \
             hipLaunchKernelGGL((trace_kernel<true, COUNT, 2>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
@@ -1577,14 +1740,12 @@ struct rt_renderer {
         if (counters) RT_TS(true); else RT_TS(false);
 #undef RT_TS
         if (!last) {
-            const int zgrid = std::max(1, std::min(blocks_for((int64_t)c.t_lg), cus * 8));
-            hipLaunchKernelGGL(zero_bytes_kernel, dim3(zgrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p);
             if (b == 0)
                 hipLaunchKernelGGL(tile_bytes_kernel<1>, dim3(sgrid), dim3(kBlock), 0, st, c.bkt.p, lv, c.gslot[cur].p,
-                                   pa.map, c.gbytes.p);
+                                   pa.map, c.gbytes.p, c.lbytes.p);
             else
                 hipLaunchKernelGGL(tile_bytes_kernel<0>, dim3(sgrid), dim3(kBlock), 0, st, c.bkt.p, lv, c.gslot[cur].p,
-                                   pa.map, c.gbytes.p);
+                                   pa.map, c.gbytes.p, c.lbytes.p);
             sorted += c.t_n;
         }
         HIPCHK(hipGetLastError());
@@ -1594,8 +1755,10 @@ struct rt_renderer {
     int tsort_back(PassCtx &c, int b) {
         hipStream_t st = c.stream;
         const PassArgs pa = tsort_args(c);
-        HIPCHK(hipStreamSynchronize(st));
-        if (b > 0) c.t_lg = *c.lg_host;             // global live count after bounce b - 1
+        if (b > 0) {                                // global live count after bounce b - 1
+            if (int rc = wait_event(c.lg_ready)) return rc;
+            c.t_lg = *c.lg_host;
+        }
         const uint64_t lg = c.t_lg;
         if (lg > 0) {
             int rc;
@@ -1616,16 +1779,17 @@ struct rt_renderer {
         }
         const int tg = c.t_tiles_g;
         const int ggrid = std::max(1, std::min((int)((lg + kSortTile - 1) / kSortTile), cus * 8));
-        const int bgrid = std::max(1, std::min(blocks_for((int64_t)lg), cus * 8));
-        // global: buckets of every live slot -> new global slots (newpos) and the next live count
-        hipLaunchKernelGGL(unbias_bytes_kernel, dim3(bgrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p, c.glive.p + 2);
-        hipLaunchKernelGGL(sort_hist_kernel, dim3(ggrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p, tg, c.sort_counts.p);
+        // global: buckets of every live slot -> new global slots of this owner's slots (newpos) and
+        // the next global live count
+        hipLaunchKernelGGL(gsort_hist_kernel, dim3(ggrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p, tg,
+                           c.sort_counts.p, c.glive.p + 2);
         hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, c.glive.p, tg,
                            c.sort_offsets.p, c.sort_totals.p, c.glive.p + 1);
-        hipLaunchKernelGGL(sort_rank_kernel, dim3(ggrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p, tg,
+        hipLaunchKernelGGL(sort_rank_kernel, dim3(ggrid), dim3(kBlock), 0, st, c.gbytes.p, c.lbytes.p, c.glive.p, tg,
                            c.sort_offsets.p, c.sort_totals.p, c.newpos.p);
         hipLaunchKernelGGL(set_count_kernel, dim3(1), dim3(64), 0, st, c.glive.p, 0u, c.glive.p + 1);
         HIPCHK(hipMemcpyAsync(c.lg_host, c.glive.p + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(c.lg_ready, st));
         // local: this owner's rays in the same stable order (local order = ascending global slot),
         // each carrying its new global slot
         const uint32_t *lv = c.live.p + b;
@@ -1759,29 +1923,54 @@ struct rt_renderer {
         if (tsort()) {
             if (!xfn) return rtamd::fail(RT_E_INVALID, "pixel tiles with sort on need the per-bounce exchange "
                                                        "(rt_renderer_set_exchange)");
-            for (int g0 = 0; g0 < count; g0 += inflight) {
-                const int gn = std::min(inflight, count - g0);
-                for (int j = 0; j < gn; j++)
-                    if (int rc = tsort_begin(ctx[j], pass_begin + (g0 + j) * stride)) return rc;
-                for (int b = 0; b < bounces; b++) {
-                    for (int j = 0; j < gn; j++)
-                        if (int rc = tsort_front(ctx[j], b, sorted)) return rc;
-                    if (b + 1 != bounces)
-                        for (int j = 0; j < gn; j++)
-                            if (int rc = tsort_back(ctx[j], b)) return rc;
+            // staggered first passes: context j starts at step j * bounces / inflight (RTAMD_TSTAGGER=0:
+            // all at step 0, i.e. the passes of a group advance together)
+            const char *stg = std::getenv("RTAMD_TSTAGGER");
+            const bool stagger = !stg || std::atoi(stg) != 0;
+            const int nc = std::min(inflight, std::max(count, 1));
+            for (int j = 0; j < nc; j++) {
+                ctx[j].t_b = -1;
+                HIPCHK(hipMemsetAsync(ctx[j].glive.p + 2, 0, sizeof(uint32_t), ctx[j].stream));   // bad bytes of the run
+            }
+            int next = 0, done = 0;
+            for (int step = 0; done < count; step++) {
+                for (int j = 0; j < nc; j++) {       // idle contexts take the next pass (pass order)
+                    PassCtx &c = ctx[j];
+                    if (c.t_b < 0 && next < count && (!stagger || step >= (int64_t)j * bounces / nc)) {
+                        if (int rc = tsort_begin(c, pass_begin + next * stride, next)) return rc;
+                        next++;
+                    }
                 }
-                for (int j = 0; j < gn; j++) {
-                    float *sums = sums_of(ctx[j], g0 + j);
-                    if (int rc = tsort_end(ctx[j], sums)) return rc;
-                    if (int rc = add_pass(ctx[j], ctx[j].t_p, sums)) return rc;
-                    uint32_t bad = 0;
-                    HIPCHK(hipMemcpyAsync(&bad, ctx[j].glive.p + 2, sizeof(bad), hipMemcpyDeviceToHost, ctx[j].stream));
-                    HIPCHK(hipStreamSynchronize(ctx[j].stream));
-                    if (bad)
-                        return rtamd::fail(RT_E_INVALID, "tile exchange: " + std::to_string(bad) +
-                                                         " global slots had no owner's byte (the exchange must sum every owner's array)");
+                for (int j = 0; j < nc; j++)
+                    if (ctx[j].t_b >= 0 && bounces > 0)
+                        if (int rc = tsort_front(ctx[j], ctx[j].t_b, sorted)) return rc;
+                for (int j = 0; j < nc; j++) {
+                    PassCtx &c = ctx[j];
+                    if (c.t_b < 0) continue;
+                    if (c.t_b + 1 < bounces) {
+                        if (int rc = tsort_back(c, c.t_b)) return rc;
+                        c.t_b++;
+                        continue;
+                    }
+                    // the pass's last bounce is enqueued: accumulate it (passes end in the order they
+                    // started, so the framebuffer adds stay in pass order)
+                    float *sums = sums_of(c, c.t_k);
+                    if (int rc = tsort_end(c, sums)) return rc;
+                    if (int rc = add_pass(c, c.t_p, sums)) return rc;
+                    c.t_b = -1;
+                    done++;
                 }
             }
+            uint32_t bad = 0;
+            for (int j = 0; j < nc; j++) {
+                uint32_t v = 0;
+                HIPCHK(hipMemcpyAsync(&v, ctx[j].glive.p + 2, sizeof(v), hipMemcpyDeviceToHost, ctx[j].stream));
+                HIPCHK(hipStreamSynchronize(ctx[j].stream));
+                bad += v;
+            }
+            if (bad)
+                return rtamd::fail(RT_E_INVALID, "tile exchange: " + std::to_string(bad) +
+                                                 " global slots had no owner's byte (the exchange must sum every owner's array)");
         } else {
             for (int k = 0; k < count; k++) {
                 PassCtx &c = ctx[k % inflight];
@@ -2052,6 +2241,47 @@ int rt_renderer_set_exchange(rt_renderer *r, rt_exchange_fn fn, void *user, int3
         const size_t n = (size_t)r->width * r->height * std::min(20, std::max(1, r->spp));
         HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&r->xhost), n));
     }
+    return RT_OK;
+}
+
+namespace {
+// The per-bounce bucket-byte exchange over the renderer's own RCCL communicator: an in-place uint8
+// sum over the owners on the pass's stream (every slot has one owner, so no byte exceeds 65).
+int rccl_exchange(void *user, uint8_t *bytes, uint64_t n, void *stream) {
+    const ncclResult_t r = ncclAllReduce(bytes, bytes, n, ncclUint8, ncclSum, static_cast<ncclComm_t>(user),
+                                         static_cast<hipStream_t>(stream));
+    return r == ncclSuccess ? 0 : -(int)r - 1;
+}
+}  // namespace
+
+int rt_rccl_unique_id(uint8_t *id_out) {
+    static_assert(sizeof(ncclUniqueId) == RT_RCCL_ID_BYTES, "RT_RCCL_ID_BYTES must match NCCL_UNIQUE_ID_BYTES");
+    if (!id_out) return rtamd::fail(RT_E_INVALID, "rt_rccl_unique_id: null output");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return rtamd::fail(RT_E_HIP, std::string("Error ncclGetUniqueId ") + ncclGetErrorString(r));
+    std::memcpy(id_out, &id, sizeof(id));
+    return RT_OK;
+}
+
+int rt_renderer_set_exchange_rccl(rt_renderer *r, const uint8_t *id, int32_t nranks, int32_t rank) {
+    if (!r || !id || nranks < 1 || rank < 0 || rank >= nranks)
+        return rtamd::fail(RT_E_INVALID, "rt_renderer_set_exchange_rccl: bad argument");
+    if (r->xcomm) return rtamd::fail(RT_E_INVALID, "rt_renderer_set_exchange_rccl: the renderer already has a communicator");
+    HIPCHK(hipSetDevice(r->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t e = ncclCommInitRank(&comm, nranks, uid, rank);
+    if (e != ncclSuccess) return rtamd::fail(RT_E_HIP, std::string("Error ncclCommInitRank ") + ncclGetErrorString(e));
+    r->xcomm = comm;
+    return rt_renderer_set_exchange(r, rccl_exchange, comm, 1);
+}
+
+int rtamd_renderer_set_poll(rt_renderer *r, int (*fn)(void *), void *user) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    r->xpoll = fn;
+    r->xpoll_user = user;
     return RT_OK;
 }
 

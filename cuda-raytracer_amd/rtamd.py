@@ -259,6 +259,18 @@ def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=
     return fb, st.as_dict()
 
 
+RCCL_ID_BYTES = 128   # RT_RCCL_ID_BYTES
+
+
+def rccl_unique_id():
+    """rt_rccl_unique_id: a new RCCL communicator id (bytes) for set_exchange_rccl."""
+    buf = (C.c_uint8 * RCCL_ID_BYTES)()
+    f = lib().rt_rccl_unique_id
+    f.argtypes = [P]
+    _check(f(buf))
+    return bytes(buf)
+
+
 def trace_rays(scene, rays, device=0, counters=False):
     """rt_trace_rays: closest hit of rays (n, 6) float32 {o.xyz, d.xyz}.  Returns (t, index, stats)."""
     rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
@@ -294,9 +306,19 @@ class Renderer:
         _check(lib().rt_renderer_run_host(self.h, pass_begin, count, stride, _ptr(out), C.byref(st)))
         return out, st.as_dict()
 
-    def set_exchange(self, exchange):
-        """Pixel tiles with sort on: exchange(arr) must sum the uint8 numpy array over all tile
-        owners in place (rt_renderer_set_exchange with a host buffer)."""
+    def set_exchange(self, exchange=None, c_fn=None, user=None):
+        """Pixel tiles with sort on (rt_renderer_set_exchange).  Either
+        exchange(arr): sums the uint8 numpy array over all tile owners in place (host buffer,
+        on_device = 0), or c_fn/user: a native rt_exchange_fn (a ctypes function pointer, e.g. from
+        a loaded library) called with the device pointer and the pass's HIP stream (on_device = 1),
+        which must enqueue its in-place sum on that stream."""
+        f = lib().rt_renderer_set_exchange
+        if c_fn is not None:
+            f.argtypes = [P, P, P, I32]
+            self._exchange = (c_fn, user)   # kept alive as long as the renderer
+            _check(f(self.h, C.cast(c_fn, P), P(user) if user else None, 1))
+            return
+
         def cb(user, p, n, stream):
             try:
                 exchange(np.ctypeslib.as_array(p, shape=(int(n),)))
@@ -304,9 +326,17 @@ class Renderer:
             except Exception:           # reported by the renderer as a failed exchange
                 return -1
         self._exchange = EXCHANGE(cb)  # kept alive as long as the renderer
-        f = lib().rt_renderer_set_exchange
         f.argtypes = [P, EXCHANGE, P, I32]
         _check(f(self.h, self._exchange, None, 0))
+
+    def set_exchange_rccl(self, unique_id, nranks, rank):
+        """The exchange over an RCCL communicator the renderer joins (one process per GPU):
+        rt_renderer_set_exchange_rccl.  unique_id: the RT_RCCL_ID_BYTES bytes rank 0 got from
+        rccl_unique_id(), the same on every rank.  Blocks until every rank has joined."""
+        f = lib().rt_renderer_set_exchange_rccl
+        f.argtypes = [P, P, I32, I32]
+        buf = (C.c_uint8 * RCCL_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        _check(f(self.h, buf, int(nranks), int(rank)))
 
     def set_counters(self, on):
         _check(lib().rt_renderer_set_counters(self.h, int(on)))

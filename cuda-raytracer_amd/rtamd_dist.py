@@ -128,7 +128,7 @@ def tile_rows(height: int, world: int, rank: int, rows: int = 8) -> List[int]:
 
 
 class TileShardedFrame:
-    """Pixel-tile sharding, exact with sort off.
+    """Pixel-tile sharding, exact with sort on and off.
 
     Every rank renders every pass, but only the rays of its own row stripes (stripes of `rows`
     rows dealt round-robin, so sky rows and geometry rows spread over the ranks), with their
@@ -136,9 +136,11 @@ class TileShardedFrame:
     ((0 + S_0) + S_1) + ..., bit for bit.  `render_tile(out)` renders the rank's share of the
     frame and writes the rank's framebuffer (W*H*3 float32, other ranks' rows 0) into `out`.
     `collect()` packs the owned rows and gathers them to rank 0 over RCCL (one gather of the
-    framebuffer, 24.9 MB at 1080p); rank 0 puts them back in place.  No per-bounce collective.
-    With sort on the process seeds follow the global post-sort slot (raytracing.cu:89), which
-    a tile cannot know: use PassShardedFrame there.
+    framebuffer, 24.9 MB at 1080p); rank 0 puts them back in place.  With sort off there is no
+    per-bounce collective.  With sort on the process seeds follow the global post-sort slot
+    (raytracing.cu:89): the renderer needs the per-bounce bucket-byte exchange first
+    (`join_tile_exchange`, an in-place RCCL all-reduce on the device inside the library; the gloo
+    tests use `bucket_exchange` with the oracle's restatement).
     """
 
     def __init__(self, dist, torch, width: int, height: int, device, render_tile: Callable, rows: int = 8):
@@ -186,12 +188,23 @@ class TileShardedFrame:
         return self.collect()
 
 
+def join_tile_exchange(dist, renderer, rtamd):
+    """Pixel tiles with the reorder on, one process per GPU: the renderer joins an RCCL communicator
+    of its own over the process group's ranks (rank 0 makes the id, a torch.distributed broadcast
+    hands it to the others) and sums the bucket bytes with an in-place ncclAllReduce on each pass's
+    stream (rt_renderer_set_exchange_rccl): no byte leaves the device, no Python per bounce."""
+    holder = [rtamd.rccl_unique_id() if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(holder, src=0)
+    renderer.set_exchange_rccl(holder[0], dist.get_world_size(), dist.get_rank())
+
+
 def bucket_exchange(dist, torch):
     """The per-bounce exchange of pixel-tile sharding with the reorder on: every
     owner writes bucket + 1 at the global slot of each of its live rays into a zeroed byte array;
     the sum over owners (one all-reduce, uint8: each slot has exactly one owner, so no byte
     exceeds 65) gives every owner the whole bucket array, from which it ranks its own rays.
-    Returns exchange(arr): in-place sum of a numpy uint8 array over the process group."""
+    Returns exchange(arr): in-place sum of a numpy uint8 array over the process group (host
+    memory: the gloo tests of the oracle's restatement; GPU renderers use join_tile_exchange)."""
     def exchange(arr):
         t = torch.from_numpy(arr)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum {
     RT_OK = 0,
@@ -195,6 +195,16 @@ int rt_renderer_clear(rt_renderer *r);                               /* zero the
  * (pass by pass of a group in flight, bounce by bounce).  Without an exchange such a render fails. */
 typedef int (*rt_exchange_fn)(void *user, uint8_t *bytes, uint64_t n, void *hip_stream);
 int rt_renderer_set_exchange(rt_renderer *r, rt_exchange_fn fn, void *user, int32_t on_device);
+/* The same exchange over RCCL for one process per GPU (torchrun-style hosts): the renderer joins
+ * an RCCL communicator of nranks owners (ncclCommInitRank; blocks until every rank has joined) and
+ * sums the bytes with an in-place ncclAllReduce(uint8) on the pass's stream, so no byte leaves
+ * the device.  Every rank passes the same RT_RCCL_ID_BYTES-byte id: rank 0 makes it with
+ * rt_rccl_unique_id and the host hands it to the others (e.g. a torch.distributed broadcast).
+ * The communicator is the renderer's and is destroyed with it.  No reference counterpart: the
+ * reference ran one device (raytracing.cu:170-284). */
+#define RT_RCCL_ID_BYTES 128
+int rt_rccl_unique_id(uint8_t *id_out);
+int rt_renderer_set_exchange_rccl(rt_renderer *r, const uint8_t *id, int32_t nranks, int32_t rank);
 int rt_renderer_set_counters(rt_renderer *r, int32_t enable);
 /* Per-bounce HIP events behind rt_stats.process_ms / sort_ms (default on).  Off, those stay 0 and
  * a pass's stream carries no marker packets between its kernels (~2 % faster frames). */

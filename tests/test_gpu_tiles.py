@@ -82,24 +82,24 @@ def test_tiles_with_sort_on_need_an_exchange(gpu):
         R.render(psc, sort=False, tiles=(2, 2))
 
 
-@pytest.mark.parametrize("scene,image,rows,owners", [("cornell_plus", (48, 40, 45, 6), 8, 2),
-                                                     ("teapot", (64, 36, 20, 16), 4, 3),
-                                                     ("spheres", (40, 24, 20, 8), 8, 2)])
-def test_tiles_with_sort_on_bitexact(scene, image, rows, owners):
-    """Pixel tiles WITH the reorder on: `owners` renderers on this GPU, one per tile
-    owner, each in its own thread, exchange one byte per global live ray after every bounce but the
-    last (rt_renderer_set_exchange; here a host-side sum over the owners, RCCL's ncclAllReduce in
-    the multi-GPU library path) and rank their rays by the global stable order.  Their framebuffers
-    (disjoint pixels) add up to the oracle's single-process render bit for bit, and the live segment
-    counts add up to the oracle's."""
+SORT_ON_CASES = [("cornell_plus", (48, 40, 45, 6), 8, 2),
+                 ("teapot", (64, 36, 20, 16), 4, 3),
+                 ("spheres", (40, 24, 20, 8), 8, 2),
+                 ("lamp_available", (48, 27, 20, 32), 4, 3),
+                 ("cornell", (24, 16, 8, 4), 8, 3)]      # 2 stripes, 3 owners: owner 2 has none
+
+
+def render_owners(path, image, rows, owners, exchange):
+    """`owners` tile renderers on this GPU, one per tile owner, each in its own thread, with sort on;
+    exchange = "host" (a numpy sum through the host-buffer callback) or "device" (the device-side
+    group sum of tests/native/xchg.hip on the pass streams, the stream contract of the library's
+    RCCL path).  Returns the owners' framebuffers summed (disjoint pixels) and their stats."""
     import threading
-    if R.device_count() < 1:
-        pytest.fail("no HIP device visible: the GPU tests must run on the MI355X box")
-    path = "%s/%s.scene" % (R.ASSETS, scene)
-    ref, rst = O.OracleScene(path, image=image).render(sort=True)
+    import xchg_lib
     sc = R.Scene(path, image=image)
     bar = threading.Barrier(owners, timeout=60)
     parts, out, errs = {}, {}, []
+    group = xchg_lib.Group(owners) if exchange == "device" else None
 
     def exchange_for(i):
         def ex(arr):
@@ -113,7 +113,10 @@ def test_tiles_with_sort_on_bitexact(scene, image, rows, owners):
     def run(i):
         try:
             r = R.Renderer(sc, sort=True, tiles=(owners, i, rows))
-            r.set_exchange(exchange_for(i))
+            if group:
+                group.attach(r, i)
+            else:
+                r.set_exchange(exchange_for(i))
             st = r.run(pass_begin=0, count=-1)
             out[i] = (r.framebuffer(), st)
             r.close()
@@ -125,9 +128,60 @@ def test_tiles_with_sort_on_bitexact(scene, image, rows, owners):
         t.start()
     for t in th:
         t.join(timeout=300)
+    if group:
+        group.close()
     assert not errs, errs
-    fb = np.zeros_like(ref)
-    for i in range(owners):
-        fb = fb + out[i][0]
+    fb = sum(out[i][0] for i in range(owners))
+    return fb, [out[i][1] for i in range(owners)]
+
+
+@pytest.mark.parametrize("exchange", ["host", "device"])
+@pytest.mark.parametrize("scene,image,rows,owners", SORT_ON_CASES)
+def test_tiles_with_sort_on_bitexact(gpu, scene, image, rows, owners, exchange):
+    """Pixel tiles WITH the reorder on: `owners` renderers on this GPU exchange one byte
+    per global live ray after every bounce but the last (rt_renderer_set_exchange) and rank their
+    rays by the global stable order.  Their framebuffers (disjoint pixels) add up to the oracle's
+    single-process render bit for bit, and the live segment counts add up to the oracle's.  The
+    "device" exchange runs on the pass streams with the renderer waiting only for the live-count
+    copy of the previous bounce (rt_render.hip tsort_back), as the RCCL exchange does."""
+    path = "%s/%s.scene" % (R.ASSETS, scene)
+    ref, rst = O.OracleScene(path, image=image).render(sort=True)
+    fb, sts = render_owners(path, image, rows, owners, exchange)
     assert np.array_equal(fb, ref)
-    assert sum(out[i][1]["live_segments"] for i in range(owners)) == rst["live_segments"]
+    assert sum(s["live_segments"] for s in sts) == rst["live_segments"]
+
+
+def test_tiles_with_sort_on_all_passes_together(gpu, monkeypatch):
+    """RTAMD_TSTAGGER=0: every context's first pass starts at step 0 (no staggering); same image."""
+    monkeypatch.setenv("RTAMD_TSTAGGER", "0")
+    path = "%s/teapot.scene" % R.ASSETS
+    image = (40, 24, 65, 8)
+    ref, _ = O.OracleScene(path, image=image).render(sort=True)
+    fb, _ = render_owners(path, image, 4, 2, "device")
+    assert np.array_equal(fb, ref)
+
+
+@pytest.mark.parametrize("sort", [True, False])
+def test_library_tile_shard_one_device(gpu, sort):
+    """rt_render with device_count = 1 and shard_tiles = 1 (rt_multi.hip run_device_tiles: the RCCL
+    communicator, the renderer, the ncclReduce of the framebuffer) equals the oracle bit for bit."""
+    path = "%s/teapot.scene" % R.ASSETS
+    image = (48, 30, 45, 8)
+    ref, _ = O.OracleScene(path, image=image).render(sort=sort)
+    fb, st = R.render(R.Scene(path, image=image), sort=sort, devices=[0], shard_tiles=True)
+    assert np.array_equal(fb, ref)
+    assert st["passes"] == 3
+
+
+@pytest.mark.parametrize("shard_tiles", [False, True])
+def test_multi_device_failure_after_setup_returns(gpu, monkeypatch, shard_tiles):
+    """A device failing after the setup barrier (RTAMD_FAIL_AFTER_SETUP) makes rt_render return its
+    error; the device aborts only its own communicator (no call can race the abort)."""
+    monkeypatch.setenv("RTAMD_FAIL_AFTER_SETUP", "0")
+    psc = R.Scene("%s/cornell.scene" % R.ASSETS, image=(32, 32, 8, 2))
+    with pytest.raises(R.RtError, match="injected failure"):
+        R.render(psc, sort=True, devices=[0], shard_tiles=shard_tiles)
+    monkeypatch.delenv("RTAMD_FAIL_AFTER_SETUP")
+    fb, _ = R.render(psc, sort=True, devices=[0], shard_tiles=shard_tiles)   # the library still works
+    ref, _ = O.OracleScene("%s/cornell.scene" % R.ASSETS, image=(32, 32, 8, 2)).render(sort=True)
+    assert np.array_equal(fb, ref)

@@ -120,6 +120,13 @@ def main():
             rec["trace_read_bytes_per_launch"] = int(rd / n_trace)
             rec["trace_write_bytes_per_launch"] = int(wr / n_trace)
             rec["trace_fetch_size_bytes_per_launch"] = int(total(trace, "fetch_size_bytes") / n_trace)
+            # exclusive launch durations of the same profiled run (the profiler serialises dispatches),
+            # in dispatch order per trace kernel variant: the denominator of the fabric-bytes rate
+            durs = [round(d["dur_ms"], 5) for (k, _), d in disp.items() if k in trace and "dur_ms" in d]
+            if durs:
+                rec["trace_dur_ms_per_launch"] = durs
+                rec["trace_dur_ms_avg"] = sum(durs) / len(durs)
+                rec["trace_fabric_gbs"] = (rd + wr) / n_trace / (rec["trace_dur_ms_avg"] / 1e3) / 1e9
             rd, wr = hbm(list(summary))
             rec["pass_bytes"] = int((rd + wr) / passes)
             rec["note"] = ("trace_bytes_per_launch: summed over every trace_kernel dispatch of the profiled passes and "
