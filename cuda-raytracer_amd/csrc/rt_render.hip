@@ -108,7 +108,37 @@ struct DevScene {
     uint32_t root_ref;
     V3 cam, tl, sr, su, min_coord, inv_dim;
     float inv_w, inv_h;
+    V3 co_lo, co_scale;               // coherence key: origin -> [0, 4) cells of the scene box (trace order only)
 };
+
+// ---------------------------------------------------------------- trace order (coherence)
+// The trace of a bounce may visit the live slots in ANY order: each slot's closest hit depends on
+// its ray alone, and the refill queue only decides which lane traces which slot.  The reference
+// order of the slots (the stable sort by the 6-bit key, raytracing.cu:238-247) is what the seeds
+// follow, so the state stays in that order; the trace instead reads its slots through a
+// permutation that groups, within windows of consecutive slots, rays of the same direction octant
+// and origin cell, so the 64 lanes of a wave start near each other going the same way (shared
+// node fetches, fewer divergent leaf/internal steps).  Round 3.
+#ifndef RT_COHERENT
+#define RT_COHERENT 0
+#endif
+#ifndef RT_CWIN
+#define RT_CWIN 8192                  // slots per window of the trace-order permutation
+#endif
+constexpr int kCoWin = RT_CWIN;
+constexpr int kCoKeys = 256;
+// 8-bit key: direction octant (3 bits, high) then a 5-bit Morton code of the origin's cell in a
+// 4 x 2 x 4 grid over the scene box (x and z two bits, y one).  NaN / out-of-box origins clamp.
+__device__ __forceinline__ uint32_t coherence_key(V3 o, V3 d, V3 lo, V3 scale) {
+    auto cell = [](float v, float lim) -> uint32_t {
+        return v > 0.0f ? (uint32_t)fminf(v, lim) : 0u;   // NaN -> 0
+    };
+    const uint32_t cx = cell((o.x - lo.x) * scale.x, 3.0f), cy = cell((o.y - lo.y) * scale.y * 0.5f, 1.0f),
+                   cz = cell((o.z - lo.z) * scale.z, 3.0f);
+    const uint32_t oct = (d.x < 0.0f ? 4u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 1u : 0u);
+    const uint32_t morton = ((cz >> 1) << 4) | ((cx >> 1) << 3) | (cy << 2) | ((cz & 1u) << 1) | (cx & 1u);
+    return (oct << 5) | morton;
+}
 
 #ifdef RT_PROFILE
 // Wave-level traversal profile (debug builds only): see tools/variants.sh + RT_PROFILE=1.
@@ -230,16 +260,10 @@ __device__ __forceinline__ void slab_pair(float4 a, float4 b, float4 c, V3 o, fl
 // Möller–Trumbore (scene.cu:160-195, rt_device.h ray_triangle) with the early-outs folded into one
 // predicate: every quantity is computed for every lane and the accept test is the conjunction of
 // the reference's four reject tests, negated exactly as written (a NaN u, v or t rejects nothing,
-// as in the branchy form).  Same values, same outcome; no divergent exec-mask regions.
-#ifndef RT_MT_FLAT
-#define RT_MT_FLAT 0
-#endif
-#ifndef RT_POP_FLAT
-#define RT_POP_FLAT 0
-#endif
-#ifndef RT_DESC_FLAT
-#define RT_DESC_FLAT 0
-#endif
+// as in the branchy form).  Same values, same outcome; no divergent exec-mask regions.  In a wave
+// of ~20 leaf lanes an early-out almost never skips work for all of them, so the nested branches
+// only cost their exec-mask bookkeeping (round 3, with the flat pop loop below: A/B teapot full
+// frame 6.94 -> 6.86 ms/pass over 5 rounds, 7.06 -> 6.86 over 3; 20 steps 7.24 -> 7.18, 7.27 -> 7.13).
 __device__ __forceinline__ bool ray_triangle_flat(V3 o, V3 d, V3 p1, V3 e1, V3 e2, float closest, float &t) {
     const V3 h = cross(d, e2);
     const float a = dot(h, e1);
@@ -283,13 +307,17 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #ifndef RT_SORT_GRID
 #define RT_SORT_GRID 0                // cap on the reorder's hist/scatter grid (0: 8 blocks per CU)
 #endif
+#ifndef RT_REC_MAD
+#define RT_REC_MAD 0
+#endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8)))
 template <bool SORTED, bool COUNT, int FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
-                                                       unsigned long long *__restrict__ tspan) {
+                                                       unsigned long long *__restrict__ tspan,
+                                                       const uint32_t *__restrict__ perm = nullptr) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
@@ -356,7 +384,11 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 const uint32_t r = rank_below(idle);
                 const bool take = slot < 0 && r < avail;
                 const unsigned long long took = __ballot(take);
-                if (take) { slot = (int)(q_next + r); fresh = true; }
+                if (take) {
+                    // queue position -> slot: the trace-order permutation when there is one
+                    slot = perm ? (int)perm[q_next + r] : (int)(q_next + r);
+                    fresh = true;
+                }
                 q_next += (uint32_t)__popcll(took);
                 idle &= ~took;
             }
@@ -426,7 +458,15 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         // costs one memory round trip whatever mix of leaf and internal lanes the wave holds.
         bool need = false;              // the lane needs the next node from its stack
         const bool in_leaf = ti < te;
+#if RT_REC_MAD
+        // one select per operand and one 64-bit multiply-add instead of two address computations in
+        // divergent branches
+        const char *rbase = in_leaf ? reinterpret_cast<const char *>(S.tris) : reinterpret_cast<const char *>(S.nodes);
+        const uint32_t ridx = in_leaf ? (uint32_t)ti : ref, rsz = in_leaf ? 48u : 64u;
+        const float4 *rec = reinterpret_cast<const float4 *>(rbase + (uint64_t)ridx * rsz);
+#else
         const float4 *rec = in_leaf ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4;
+#endif
         const float4 a = rec[0], b = rec[1], c = rec[2];
         const uint2 kids = *reinterpret_cast<const uint2 *>(rec + 3);   // node lanes only use it
         if (in_leaf) {
@@ -434,16 +474,10 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             const float q2 = c.x;
             if (COUNT) tt++;
             float t;
-            const bool hit = RT_MT_FLAT
-                ? ray_triangle_flat(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t)
-                : ray_triangle(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t);
-            if (RT_MT_FLAT) {
-                closest = hit ? t : closest;
-                index = hit ? S.sphere_count + ti : index;
-            } else if (hit) {
-                closest = t;
-                index = S.sphere_count + ti;
-            }
+            const bool hit =
+                ray_triangle_flat(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t);
+            closest = hit ? t : closest;
+            index = hit ? S.sphere_count + ti : index;
             need = ++ti == te;
         } else {
             if (COUNT) iv++;
@@ -479,18 +513,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             if (both) sp++;
             ref = any ? next_ref : ref;
             const bool descend = any && !(next_t >= closest);
-#if RT_DESC_FLAT
-            // entering the next node as selects; only a big leaf's range takes a (rare) branch
-            if (COUNT) pn += descend ? 1u : 0u;
-            const bool leaf = descend && (ref & kLeaf);
-            if (__builtin_expect(leaf && (ref & kBigLeaf), 0)) {
-                leaf_range(S, ref, ti, te);
-            } else {
-                ti = leaf ? (int)(ref & 0xFFFFFFu) : ti;
-                te = leaf ? ti + (int)((ref >> 24) & 0x3Fu) : te;
-            }
-            need = !descend || (leaf && ti == te);
-#else
             need = !descend;
             if (descend) {
                 if (COUNT) pn++;
@@ -499,15 +521,14 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     need = ti == te;
                 }
             }
-#endif
         }
 #ifdef RT_PROFILE
         if (__ballot(need)) PROF(5, 1);
 #endif
-#if RT_POP_FLAT
-        // The same pops as below with the per-entry decisions as selects: the LDS entry is read for
-        // every popping lane (an empty stack reads entry 0, unused), only the rare overflow-stack
-        // entries and big-leaf ranges take a branch.
+        // Pop to the next entry nearer than closest (scene.cu:147-152), the per-entry decisions as
+        // selects: the LDS entry is read for every popping lane (an empty stack reads entry 0,
+        // unused), only the rare overflow-stack entries and big-leaf ranges take a branch (round 3:
+        // the nested if/else form cost ~27 SALU + 7 branches more per loop body).
         while (need) {
             PROF(10, 1);
             const bool empty = sp == 0;
@@ -535,34 +556,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             }
             need = !empty && (!take || (leaf && ti == te));
         }
-#else
-        while (need) {                  // pop to the next entry nearer than closest
-            PROF(10, 1);
-            if (sp == 0) {
-                slot = -2 - slot;       // done; {closest, index} stored at the next refill or at exit
-                break;
-            }
-            sp--;
-            uint32_t eref;
-            float edist;
-            if (__builtin_expect(sp < kStackLds, 1)) {
-                const uint2 e = col[sp * kBlock];
-                eref = e.x;
-                edist = __uint_as_float(e.y);
-            } else {
-                eref = overflow[(sp - kStackLds) * lanes + gl];
-                edist = __uint_as_float(overflow[dist_half + (sp - kStackLds) * lanes + gl]);
-            }
-            if (edist >= closest) continue;
-            ref = eref;
-            if (COUNT) pn++;
-            need = false;
-            if (ref & kLeaf) {
-                leaf_range(S, ref, ti, te);
-                need = ti == te;
-            }
-        }
-#endif
     }
     if (slot <= -2) hits[-2 - slot] = make_float2(closest, __int_as_float(index));
     Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
@@ -845,7 +838,9 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
                                                               uint32_t *__restrict__ rid_out, SlotMap map,
                                                               const uint32_t *__restrict__ gslot_in = nullptr,
                                                               const uint32_t *__restrict__ newpos = nullptr,
-                                                              uint32_t *__restrict__ gslot_out = nullptr) {
+                                                              uint32_t *__restrict__ gslot_out = nullptr,
+                                                              uint8_t *__restrict__ ckey_out = nullptr, V3 co_lo = V3{},
+                                                              V3 co_scale = V3{}) {
     // gslot_out (pixel tiles with the reorder on): each moved ray also carries its new global slot,
     // newpos[its old global slot] (old global slot at bounce 0: the ray index, map.ray(item))
     const int n = (int)*live_count;
@@ -885,6 +880,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
             tc_out[pos] = t;
             rid_out[pos] = id;
             if (gslot_out) gslot_out[pos] = gs;
+            if (ckey_out) ckey_out[pos] = (uint8_t)coherence_key(v3(g0.x, g0.y, g0.z), v3(g0.w, g1.x, g1.y), co_lo, co_scale);
         }
         __syncthreads();
         if (threadIdx.x < kBuckets) {
@@ -1001,6 +997,47 @@ __global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__rest
         }
     }
 }
+// Trace-order permutation of the live prefix: per window of kCoWin consecutive slots, the slots
+// grouped by coherence key (counting sort in LDS; the order inside a key group is whatever the LDS
+// atomics give, which the render's result does not depend on).  perm[w + p] = slot.
+__global__ __launch_bounds__(kBlock) void window_perm_kernel(const uint8_t *__restrict__ ckey,
+                                                             const uint32_t *__restrict__ live_count,
+                                                             uint32_t *__restrict__ perm) {
+    const uint32_t n = *live_count;
+    __shared__ uint32_t cnt[kCoKeys];
+    __shared__ uint32_t wsum[kBlock / 64];
+    for (uint32_t w0 = blockIdx.x * (uint32_t)kCoWin; w0 < n; w0 += gridDim.x * (uint32_t)kCoWin) {
+        const uint32_t w1 = min(n, w0 + (uint32_t)kCoWin);
+        for (int k = threadIdx.x; k < kCoKeys; k += kBlock) cnt[k] = 0;
+        __syncthreads();
+        for (uint32_t i = w0 + threadIdx.x; i < w1; i += kBlock) atomicAdd(&cnt[ckey[i]], 1u);
+        __syncthreads();
+        static_assert(kCoKeys == kBlock, "one key per thread in the scan");
+        {   // exclusive scan of the 256 counts (one per thread)
+            const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+            const uint32_t v = cnt[threadIdx.x];
+            uint32_t x = v;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off);
+                if (lane >= off) x += y;
+            }
+            if (lane == 63) wsum[wave] = x;
+            __syncthreads();
+            uint32_t pre = 0;
+            for (int k = 0; k < wave; k++) pre += wsum[k];
+            __syncthreads();
+            cnt[threadIdx.x] = pre + x - v;
+        }
+        __syncthreads();
+        for (uint32_t i = w0 + threadIdx.x; i < w1; i += kBlock) {
+            const uint32_t p = atomicAdd(&cnt[ckey[i]], 1u);
+            perm[w0 + p] = i;
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void set_count_kernel(uint32_t *__restrict__ dst, uint32_t v, const uint32_t *__restrict__ src) {
     if (threadIdx.x == 0) *dst = src ? *src : v;
 }
@@ -1021,7 +1058,8 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
                                                                     const uint32_t *__restrict__ totals,
                                                                     float4 *__restrict__ geo_out,
                                                                     float4 *__restrict__ tc_out,
-                                                                    uint32_t *__restrict__ rid_out) {
+                                                                    uint32_t *__restrict__ rid_out,
+                                                                    uint8_t *__restrict__ ckey_out = nullptr) {
     const int n = (int)*live_count;
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
@@ -1050,6 +1088,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
                 geo_out[(size_t)pos * 2 + 1] = make_float4(sh.nd.y, sh.nd.z, sh.T.x, sh.T.y);
                 tc_out[pos] = make_float4(sh.T.z, sh.C.x, sh.C.y, sh.C.z);
                 rid_out[pos] = sh.ray;
+                if (ckey_out) ckey_out[pos] = (uint8_t)coherence_key(sh.no, sh.nd, S.co_lo, S.co_scale);
             }
             __syncthreads();
             if (threadIdx.x < kBuckets) {
@@ -1206,6 +1245,8 @@ struct PassCtx {
     DevBuf<uint32_t> rid[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
     DevBuf<uint8_t> bkt;
     DevBuf<float2> hits;
+    DevBuf<uint32_t> perm;            // trace-order permutation of the live slots (RT_COHERENT)
+    DevBuf<uint8_t> ckey;             // coherence key per slot, written by the reorder
     DevBuf<float> psum;               // this pass's per-pixel sums (when the caller gives no buffer)
     // pixel tiles with the reorder on: global slot per ray (ping-pong with the state), the global
     // bucket bytes (exchanged) and this owner's own bytes, their ranks, the global live count
@@ -1267,6 +1308,7 @@ struct rt_renderer {
     // shade/reorder (INLINE), saving the hit round trip and the trace launch per bounce.
     bool inline_hits = false;
     int fused_upto = -1;              // fused reorder at bounces <= this (when not `fused`)
+    bool coherent = RT_COHERENT != 0; // trace through a coherence-ordered permutation (RTAMD_COHERENT overrides)
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
     DevBuf<float4> spheres, tris, mats, nodes;
@@ -1344,6 +1386,8 @@ struct rt_renderer {
             fused_upto = -1;
             inline_hits = false;
         }
+        if (const char *f = std::getenv("RTAMD_COHERENT")) coherent = std::atoi(f) != 0;
+        if (tsort() || inline_hits) coherent = false;   // no trace kernel, or slots carried as data
         width = sc->width;
         height = sc->height;
         spp = sc->ray_count;
@@ -1444,7 +1488,8 @@ struct rt_renderer {
         const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
         // than half of the free device memory holds (1080p: ~2.9 GB per context).
-        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0)) +
+        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0) +
+                                                     (coherent ? 5 : 0)) +
                                  (size_t)trace_blocks_max * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
         size_t mem_free = 0, mem_total = 0;
         HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
@@ -1474,6 +1519,7 @@ struct rt_renderer {
             if ((rc = c.hits.alloc((size_t)max_rays))) return rc;
             if ((rc = c.overflow.alloc((size_t)trace_blocks_max * kBlock * 2 * (kStackMax - kStackLds)))) return rc;
             if ((rc = c.psum.alloc((size_t)pixels * 3))) return rc;
+            if (coherent && ((rc = c.perm.alloc((size_t)max_rays)) || (rc = c.ckey.alloc((size_t)max_rays)))) return rc;
             if (tsort()) {
                 for (int q = 0; q < 2; q++)
                     if ((rc = c.gslot[q].alloc((size_t)max_rays))) return rc;
@@ -1507,6 +1553,13 @@ struct rt_renderer {
         ds.inv_dim = v3(sc->inv_dimensions.x, sc->inv_dimensions.y, sc->inv_dimensions.z);
         ds.inv_w = sc->inv_width;
         ds.inv_h = sc->inv_height;
+        {   // coherence-key grid over the root box (trace order only; any box gives the same image)
+            const rt_bvh_node &r = sc->bvh[0];
+            auto sc4 = [](float lo, float hi) { return hi > lo ? 4.0f / (hi - lo) : 0.0f; };
+            ds.co_lo = v3(r.min_bound.x, r.min_bound.y, r.min_bound.z);
+            ds.co_scale = v3(sc4(r.min_bound.x, r.max_bound.x), sc4(r.min_bound.y, r.max_bound.y),
+                             sc4(r.min_bound.z, r.max_bound.z));
+        }
         HIPCHK(hipStreamSynchronize(s0));
         tm.mark("sync");
         tm.report();
@@ -1564,7 +1617,8 @@ struct rt_renderer {
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + 2 * b : nullptr); \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + 2 * b : nullptr, \
+                               (b > 0 && coherent) ? c.perm.p : nullptr);                                         \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
@@ -1611,7 +1665,8 @@ struct rt_renderer {
 #define RT_FSC2(SO, FI, IN)                                                                                      \
     hipLaunchKernelGGL((sort_scatter_shade_kernel<SO, FI, IN>), dim3(sort_grid), dim3(kBlock), 0, st, ds, pa,     \
                        c.bkt.p, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.hits.p, seed_term, lv, tiles,          \
-                       c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p)
+                       c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p,    \
+                       coherent ? c.ckey.p : nullptr)
 #define RT_FSC(SO, FI) do { if (inline_hits) RT_FSC2(SO, FI, true); else RT_FSC2(SO, FI, false); } while (0)
                     if (sort) {
                         if (b == 0) RT_FSC(true, 1); else RT_FSC(true, 0);
@@ -1620,18 +1675,29 @@ struct rt_renderer {
                     }
 #undef RT_FSC
 #undef RT_FSC2
-                } else if (b == 0 && tiled())
-                    hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
-                else if (b == 0)
-                    hipLaunchKernelGGL(sort_scatter_kernel<1>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
-                else
-                    hipLaunchKernelGGL(sort_scatter_kernel<0>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
+                } else {
+                    uint8_t *ck = coherent ? c.ckey.p : nullptr;
+                    if (b == 0 && tiled())
+                        hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                           c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                           c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, nullptr, nullptr,
+                                           nullptr, ck, ds.co_lo, ds.co_scale);
+                    else if (b == 0)
+                        hipLaunchKernelGGL(sort_scatter_kernel<1>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                           c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                           c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, nullptr, nullptr,
+                                           nullptr, ck, ds.co_lo, ds.co_scale);
+                    else
+                        hipLaunchKernelGGL(sort_scatter_kernel<0>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                           c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                           c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, nullptr, nullptr,
+                                           nullptr, ck, ds.co_lo, ds.co_scale);
+                }
+                if (coherent) {   // the next bounce's trace order
+                    const int wgrid = std::max(1, std::min((n + kCoWin - 1) / kCoWin, cus * 4));
+                    hipLaunchKernelGGL(window_perm_kernel, dim3(wgrid), dim3(kBlock), 0, st, c.ckey.p, c.live.p + b + 1,
+                                       c.perm.p);
+                }
                 HIPCHK(hipGetLastError());
                 if (pass_events) HIPCHK(hipEventRecord(s1, st));
                 cur = 1 - cur;

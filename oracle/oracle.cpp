@@ -510,10 +510,12 @@ inline bool ray_sphere(const Sphere &sp, V3 o, V3 d, float closest, float *t_out
 struct Counters {
     uint64_t pn = 0, iv = 0, tt = 0, st = 0, ht = 0, hs = 0, miss = 0, live = 0, dead = 0;
     uint32_t max_stack = 0, max_ray_pn = 0;
+    uint32_t max_ray_steps = 0;   // internal visits + triangle tests of one ray (the HIP trace's steps)
     void add(const Counters &o) {
         pn += o.pn; iv += o.iv; tt += o.tt; st += o.st; ht += o.ht; hs += o.hs; miss += o.miss;
         live += o.live; dead += o.dead; max_stack = std::max(max_stack, o.max_stack);
         max_ray_pn = std::max(max_ray_pn, o.max_ray_pn);
+        max_ray_steps = std::max(max_ray_steps, o.max_ray_steps);
     }
 };
 
@@ -615,9 +617,10 @@ void process_ray(const orc_scene *s, RayData *rp, uint32_t *key, Rng rng, bool g
         float t;
         if (ray_sphere(s->spheres[i], o, d, closest, &t)) { closest = t; index = i; }
     }
-    const uint64_t pn0 = c.pn;
+    const uint64_t pn0 = c.pn, steps0 = c.iv + c.tt;
     bvh_closest_hit(s, o, d, closest, index, c);
     c.max_ray_pn = std::max(c.max_ray_pn, (uint32_t)(c.pn - pn0));
+    c.max_ray_steps = std::max(c.max_ray_steps, (uint32_t)(c.iv + c.tt - steps0));
     if (index == -1) {
         c.miss++;
         const V3 sky = s->env[env_texel(s, d)];
@@ -722,7 +725,7 @@ int pass_total(const orc_scene *s) { return (s->ray_count + 19) / 20; }
 
 // One GPU-semantics pass: generate, bounces (process + stable sort), per-pixel ordered sum.
 void gpu_pass(const orc_scene *s, int p, bool sort, float *pass_sum, Counters &total, uint64_t *hist,
-              uint64_t *sorted, int threads) {
+              uint64_t *sorted, int threads, uint32_t *bounce_max_steps = nullptr, uint64_t *bounce_live = nullptr) {
     int rtc, rem;
     pass_params(s, p, &rtc, &rem);
     const int64_t n = (int64_t)rtc * s->width * s->height;
@@ -747,6 +750,12 @@ void gpu_pass(const orc_scene *s, int p, bool sort, float *pass_sum, Counters &t
                 xor_srand(&rng, (uint32_t)slot * 4137874753u + 279220567u * seed);
                 process_ray(s, &rays[idx[slot]], &keys[slot], rng, true, c);
             }
+        }
+        {
+            Counters bc;
+            for (auto &c : per) bc.add(c);
+            if (bounce_max_steps) bounce_max_steps[b] = bc.max_ray_steps;
+            if (bounce_live) bounce_live[b] = bc.live;
         }
         for (auto &c : per) total.add(c);
         if (hist) {
@@ -995,6 +1004,18 @@ int orc_render_tiled(const orc_scene *s, int sort, int tile_count, int tile_inde
         stats->passes = (uint32_t)pass_count;
         (void)generated;
     }
+    return 0;
+}
+
+// Per bounce of pass p (GPU semantics): the longest ray's trace steps (internal visits + triangle
+// tests, one HIP trace step each) and the live rays -- what bounds a tail bounce's latency.
+int orc_pass_bounce_profile(const orc_scene *s, int sort, int pass, uint32_t *max_steps, uint64_t *live, int threads) {
+    if (pass < 0 || pass >= pass_total(s)) { g_err = "pass range"; return -1; }
+    const int64_t pixels = (int64_t)s->width * s->height;
+    std::vector<float> sum(pixels * 3);
+    Counters total;
+    uint64_t sorted = 0;
+    gpu_pass(s, pass, sort != 0, sum.data(), total, nullptr, &sorted, threads, max_steps, live);
     return 0;
 }
 

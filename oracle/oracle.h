@@ -85,6 +85,10 @@ int orc_render_tiled(const orc_scene *s, int sort, int tile_count, int tile_inde
                      float *fb_inout, orc_stats *stats, int threads);
 int orc_render_pass_sums(const orc_scene *s, int sort, int pass_begin, int pass_count,
                          float *out, int threads);
+/* Per bounce b of pass `pass`: max_steps[b] = the longest ray's internal visits + triangle tests
+ * (the HIP trace kernel's steps), live[b] = live rays.  Arrays of `bounces` entries. */
+int orc_pass_bounce_profile(const orc_scene *s, int sort, int pass, uint32_t *max_steps, uint64_t *live,
+                            int threads);
 
 /* CPU-path semantics (raytracing.cu:122-163): bounce-invariant seed quirk, no keys,
  * no sort, sequential accumulate.  fb_out: W*H*3 (overwritten). pass_limit < 0 = all. */

@@ -82,8 +82,15 @@ __global__ void own_count_kernel(const uint8_t *__restrict__ b, uint64_t n, unsi
         own += v != 0;
         live += v >= 1 && v <= 64;
     }
-    if (own) atomicAdd(&cnt[0], (unsigned long long)own);
-    if (live) atomicAdd(&cnt[1], (unsigned long long)live);
+    // one atomic pair per wave (per-lane atomics on two words serialised the whole grid)
+    for (int off = 32; off > 0; off >>= 1) {
+        own += __shfl_xor(own, off);
+        live += __shfl_xor(live, off);
+    }
+    if ((threadIdx.x & 63) == 0 && own) {
+        atomicAdd(&cnt[0], (unsigned long long)own);
+        atomicAdd(&cnt[1], (unsigned long long)live);
+    }
 }
 
 __device__ __forceinline__ uint32_t mix(uint32_t x) {

@@ -58,6 +58,7 @@ def lib():
                                        C.c_int]
         L.orc_render_cpu_path.argtypes = [P, P, C.c_int, C.c_int, P]
         L.orc_closest_hit.argtypes = [P, P, C.c_int, P, P, P]
+        L.orc_pass_bounce_profile.argtypes = [P, C.c_int, C.c_int, P, P, C.c_int]
         L.orc_bloom.argtypes = [P, C.c_int, C.c_int, C.c_float, C.c_int]
         L.orc_tonemap.argtypes = [P, C.c_int, C.c_int, C.c_float, C.c_int, P]
         L.orc_pcg_stream.argtypes = [C.c_uint32, C.c_int, P]
@@ -137,6 +138,16 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(lib().orc_last_error().decode())
         return (fb, st.as_dict(), h) if hist else (fb, st.as_dict())
+
+    def bounce_profile(self, sort=True, pass_index=0, threads=0):
+        """Per bounce of one pass: (longest ray's trace steps = internal visits + triangle tests,
+        live rays) -- orc_pass_bounce_profile."""
+        steps = np.zeros(self.info.bounces, np.uint32)
+        live = np.zeros(self.info.bounces, np.uint64)
+        rc = lib().orc_pass_bounce_profile(self.h, int(sort), pass_index, ptr(steps), ptr(live), threads)
+        if rc:
+            raise RuntimeError(lib().orc_last_error().decode())
+        return steps, live
 
     def pass_sums(self, sort=True, pass_begin=0, pass_count=1, threads=0):
         out = np.zeros((pass_count, self.pixels * 3), np.float32)
