@@ -108,37 +108,8 @@ struct DevScene {
     uint32_t root_ref;
     V3 cam, tl, sr, su, min_coord, inv_dim;
     float inv_w, inv_h;
-    V3 co_lo, co_scale;               // coherence key: origin -> [0, 4) cells of the scene box (trace order only)
 };
 
-// ---------------------------------------------------------------- trace order (coherence)
-// The trace of a bounce may visit the live slots in ANY order: each slot's closest hit depends on
-// its ray alone, and the refill queue only decides which lane traces which slot.  The reference
-// order of the slots (the stable sort by the 6-bit key, raytracing.cu:238-247) is what the seeds
-// follow, so the state stays in that order; the trace instead reads its slots through a
-// permutation that groups, within windows of consecutive slots, rays of the same direction octant
-// and origin cell, so the 64 lanes of a wave start near each other going the same way (shared
-// node fetches, fewer divergent leaf/internal steps).  Round 3.
-#ifndef RT_COHERENT
-#define RT_COHERENT 0
-#endif
-#ifndef RT_CWIN
-#define RT_CWIN 8192                  // slots per window of the trace-order permutation
-#endif
-constexpr int kCoWin = RT_CWIN;
-constexpr int kCoKeys = 256;
-// 8-bit key: direction octant (3 bits, high) then a 5-bit Morton code of the origin's cell in a
-// 4 x 2 x 4 grid over the scene box (x and z two bits, y one).  NaN / out-of-box origins clamp.
-__device__ __forceinline__ uint32_t coherence_key(V3 o, V3 d, V3 lo, V3 scale) {
-    auto cell = [](float v, float lim) -> uint32_t {
-        return v > 0.0f ? (uint32_t)fminf(v, lim) : 0u;   // NaN -> 0
-    };
-    const uint32_t cx = cell((o.x - lo.x) * scale.x, 3.0f), cy = cell((o.y - lo.y) * scale.y * 0.5f, 1.0f),
-                   cz = cell((o.z - lo.z) * scale.z, 3.0f);
-    const uint32_t oct = (d.x < 0.0f ? 4u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 1u : 0u);
-    const uint32_t morton = ((cz >> 1) << 4) | ((cx >> 1) << 3) | (cy << 2) | ((cz & 1u) << 1) | (cx & 1u);
-    return (oct << 5) | morton;
-}
 
 #ifdef RT_PROFILE
 // Wave-level traversal profile (debug builds only): see tools/variants.sh + RT_PROFILE=1.
@@ -264,10 +235,25 @@ __device__ __forceinline__ void slab_pair(float4 a, float4 b, float4 c, V3 o, fl
 // of ~20 leaf lanes an early-out almost never skips work for all of them, so the nested branches
 // only cost their exec-mask bookkeeping (round 3, with the flat pop loop below: A/B teapot full
 // frame 6.94 -> 6.86 ms/pass over 5 rounds, 7.06 -> 6.86 over 3; 20 steps 7.24 -> 7.18, 7.27 -> 7.13).
+#ifndef RT_MT_RCP
+#define RT_MT_RCP 0
+#endif
+// 1/a bit-identical to the IEEE quotient: v_rcp_f32 and one FMA Newton step are correctly rounded for
+// every |a| in [2^-125, 2^125] on gfx950 (all 2^32 inputs checked, tools/experiments/rcp_check.hip);
+// a wave with a lane outside that range (zero, denormal, huge, inf, NaN) divides for those lanes.
+// 3 dependent VALU instead of the division's ~10.
+__device__ __forceinline__ float recip_exact(float a) {
+    const float r = __builtin_amdgcn_rcpf(a);
+    const float r1 = __builtin_fmaf(__builtin_fmaf(-a, r, 1.0f), r, r);
+    const float aa = __builtin_fabsf(a);
+    const bool ok = aa >= 0x1p-125f && aa <= 0x1p125f;
+    if (__builtin_expect(__ballot(!ok) != 0, 0)) return ok ? r1 : 1.0f / a;
+    return r1;
+}
 __device__ __forceinline__ bool ray_triangle_flat(V3 o, V3 d, V3 p1, V3 e1, V3 e2, float closest, float &t) {
     const V3 h = cross(d, e2);
     const float a = dot(h, e1);
-    const float f = 1 / a;
+    const float f = RT_MT_RCP ? recip_exact(a) : 1 / a;
     const V3 s = o - p1;
     const float u = dot(s, h) * f;
     const V3 q = cross(s, e1);
@@ -307,8 +293,8 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #ifndef RT_SORT_GRID
 #define RT_SORT_GRID 0                // cap on the reorder's hist/scatter grid (0: 8 blocks per CU)
 #endif
-#ifndef RT_REC_MAD
-#define RT_REC_MAD 0
+#ifndef RT_PRED_STEP
+#define RT_PRED_STEP 0                // 1: leaf and node bodies as one predicated block; 2: only in mixed waves
 #endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8)))
 template <bool SORTED, bool COUNT, int FIRST>
@@ -316,8 +302,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
-                                                       unsigned long long *__restrict__ tspan,
-                                                       const uint32_t *__restrict__ perm = nullptr) {
+                                                       unsigned long long *__restrict__ tspan) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
@@ -384,11 +369,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 const uint32_t r = rank_below(idle);
                 const bool take = slot < 0 && r < avail;
                 const unsigned long long took = __ballot(take);
-                if (take) {
-                    // queue position -> slot: the trace-order permutation when there is one
-                    slot = perm ? (int)perm[q_next + r] : (int)(q_next + r);
-                    fresh = true;
-                }
+                if (take) { slot = (int)(q_next + r); fresh = true; }
                 q_next += (uint32_t)__popcll(took);
                 idle &= ~took;
             }
@@ -458,17 +439,64 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         // costs one memory round trip whatever mix of leaf and internal lanes the wave holds.
         bool need = false;              // the lane needs the next node from its stack
         const bool in_leaf = ti < te;
-#if RT_REC_MAD
-        // one select per operand and one 64-bit multiply-add instead of two address computations in
-        // divergent branches
-        const char *rbase = in_leaf ? reinterpret_cast<const char *>(S.tris) : reinterpret_cast<const char *>(S.nodes);
-        const uint32_t ridx = in_leaf ? (uint32_t)ti : ref, rsz = in_leaf ? 48u : 64u;
-        const float4 *rec = reinterpret_cast<const float4 *>(rbase + (uint64_t)ridx * rsz);
-#else
         const float4 *rec = in_leaf ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4;
-#endif
         const float4 a = rec[0], b = rec[1], c = rec[2];
         const uint2 kids = *reinterpret_cast<const uint2 *>(rec + 3);   // node lanes only use it
+#if RT_PRED_STEP
+        // Both interpretations of the record for every lane, merged with selects: a wave whose lanes
+        // are partly at leaves and partly at internal nodes (nearly every wave of an incoherent
+        // bounce) ran the two bodies one after the other under exec masks; as one basic block their
+        // two dependency chains (the Möller–Trumbore division, the slab min/max tree) interleave.
+        if (RT_PRED_STEP == 1 || (__ballot(in_leaf) != 0 && __ballot(!in_leaf) != 0)) {
+            float t;
+            const bool thit =
+                ray_triangle_flat(o, d, v3(a.x, a.y, a.z), v3(a.w, b.x, b.y), v3(b.z, b.w, c.x), closest, t);
+            float t0, t1;
+            bool h0, h1;
+            slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
+            if (__builtin_expect(wave_nonfinite, 0)) {
+                float u0, u1;
+                const bool g0 = slab(a.x, a.z, b.x, b.z, c.x, c.z, o, ix, iy, iz, closest, u0);
+                const bool g1 = slab(a.y, a.w, b.y, b.w, c.y, c.w, o, ix, iy, iz, closest, u1);
+                if (!finite_inv) { h0 = g0; h1 = g1; t0 = u0; t1 = u1; }
+            }
+            const bool both = h0 && h1, any = h0 || h1;
+            const bool sel1 = h1 && (!h0 || t0 < t1);
+            const uint32_t next_ref = sel1 ? kids.y : kids.x, near_ref = sel1 ? kids.x : kids.y;
+            const float next_t = sel1 ? t1 : t0, near_t = sel1 ? t0 : t1;
+            // every lane writes the entry above its top (a leaf lane's sp does not move, so its write
+            // is overwritten before it is ever read); only a node lane with two hits pushes
+            col[min(sp, kStackLds) * kBlock] = make_uint2(near_ref, __float_as_uint(near_t));
+            const bool push = !in_leaf && both;
+            if (__builtin_expect(push && sp >= kStackLds, 0)) {
+                overflow[(sp - kStackLds) * lanes + gl] = near_ref;
+                overflow[dist_half + (sp - kStackLds) * lanes + gl] = __float_as_uint(near_t);
+            }
+            if (COUNT) {
+                tt += in_leaf ? 1u : 0u;
+                iv += in_leaf ? 0u : 1u;
+            }
+            const bool lhit = in_leaf && thit;    // leaf lanes: the triangle's outcome
+            closest = lhit ? t : closest;
+            index = lhit ? S.sphere_count + ti : index;
+            sp += push ? 1 : 0;                   // node lanes: the next child
+            const uint32_t nref = any ? next_ref : ref;
+            const bool descend = !in_leaf && any && !(next_t >= closest);
+            ref = in_leaf ? ref : nref;
+            if (COUNT) pn += descend ? 1u : 0u;
+            const bool dleaf = descend && (nref & kLeaf);
+            int nti = in_leaf ? ti + 1 : ti, nte = te;
+            if (__builtin_expect(dleaf && (nref & kBigLeaf), 0)) {
+                leaf_range(S, nref, nti, nte);
+            } else {
+                nti = dleaf ? (int)(nref & 0xFFFFFFu) : nti;
+                nte = dleaf ? nti + (int)((nref >> 24) & 0x3Fu) : nte;
+            }
+            need = in_leaf ? nti == te : (!descend || (dleaf && nti == nte));
+            ti = nti;
+            te = nte;
+        } else
+#endif
         if (in_leaf) {
             const float4 q0 = a, q1 = b;
             const float q2 = c.x;
@@ -838,9 +866,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
                                                               uint32_t *__restrict__ rid_out, SlotMap map,
                                                               const uint32_t *__restrict__ gslot_in = nullptr,
                                                               const uint32_t *__restrict__ newpos = nullptr,
-                                                              uint32_t *__restrict__ gslot_out = nullptr,
-                                                              uint8_t *__restrict__ ckey_out = nullptr, V3 co_lo = V3{},
-                                                              V3 co_scale = V3{}) {
+                                                              uint32_t *__restrict__ gslot_out = nullptr) {
     // gslot_out (pixel tiles with the reorder on): each moved ray also carries its new global slot,
     // newpos[its old global slot] (old global slot at bounce 0: the ray index, map.ray(item))
     const int n = (int)*live_count;
@@ -880,7 +906,6 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
             tc_out[pos] = t;
             rid_out[pos] = id;
             if (gslot_out) gslot_out[pos] = gs;
-            if (ckey_out) ckey_out[pos] = (uint8_t)coherence_key(v3(g0.x, g0.y, g0.z), v3(g0.w, g1.x, g1.y), co_lo, co_scale);
         }
         __syncthreads();
         if (threadIdx.x < kBuckets) {
@@ -997,47 +1022,6 @@ __global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__rest
         }
     }
 }
-// Trace-order permutation of the live prefix: per window of kCoWin consecutive slots, the slots
-// grouped by coherence key (counting sort in LDS; the order inside a key group is whatever the LDS
-// atomics give, which the render's result does not depend on).  perm[w + p] = slot.
-__global__ __launch_bounds__(kBlock) void window_perm_kernel(const uint8_t *__restrict__ ckey,
-                                                             const uint32_t *__restrict__ live_count,
-                                                             uint32_t *__restrict__ perm) {
-    const uint32_t n = *live_count;
-    __shared__ uint32_t cnt[kCoKeys];
-    __shared__ uint32_t wsum[kBlock / 64];
-    for (uint32_t w0 = blockIdx.x * (uint32_t)kCoWin; w0 < n; w0 += gridDim.x * (uint32_t)kCoWin) {
-        const uint32_t w1 = min(n, w0 + (uint32_t)kCoWin);
-        for (int k = threadIdx.x; k < kCoKeys; k += kBlock) cnt[k] = 0;
-        __syncthreads();
-        for (uint32_t i = w0 + threadIdx.x; i < w1; i += kBlock) atomicAdd(&cnt[ckey[i]], 1u);
-        __syncthreads();
-        static_assert(kCoKeys == kBlock, "one key per thread in the scan");
-        {   // exclusive scan of the 256 counts (one per thread)
-            const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-            const uint32_t v = cnt[threadIdx.x];
-            uint32_t x = v;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(x, off);
-                if (lane >= off) x += y;
-            }
-            if (lane == 63) wsum[wave] = x;
-            __syncthreads();
-            uint32_t pre = 0;
-            for (int k = 0; k < wave; k++) pre += wsum[k];
-            __syncthreads();
-            cnt[threadIdx.x] = pre + x - v;
-        }
-        __syncthreads();
-        for (uint32_t i = w0 + threadIdx.x; i < w1; i += kBlock) {
-            const uint32_t p = atomicAdd(&cnt[ckey[i]], 1u);
-            perm[w0 + p] = i;
-        }
-        __syncthreads();
-    }
-}
-
 __global__ void set_count_kernel(uint32_t *__restrict__ dst, uint32_t v, const uint32_t *__restrict__ src) {
     if (threadIdx.x == 0) *dst = src ? *src : v;
 }
@@ -1058,8 +1042,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
                                                                     const uint32_t *__restrict__ totals,
                                                                     float4 *__restrict__ geo_out,
                                                                     float4 *__restrict__ tc_out,
-                                                                    uint32_t *__restrict__ rid_out,
-                                                                    uint8_t *__restrict__ ckey_out = nullptr) {
+                                                                    uint32_t *__restrict__ rid_out) {
     const int n = (int)*live_count;
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
@@ -1088,7 +1071,6 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
                 geo_out[(size_t)pos * 2 + 1] = make_float4(sh.nd.y, sh.nd.z, sh.T.x, sh.T.y);
                 tc_out[pos] = make_float4(sh.T.z, sh.C.x, sh.C.y, sh.C.z);
                 rid_out[pos] = sh.ray;
-                if (ckey_out) ckey_out[pos] = (uint8_t)coherence_key(sh.no, sh.nd, S.co_lo, S.co_scale);
             }
             __syncthreads();
             if (threadIdx.x < kBuckets) {
@@ -1245,8 +1227,6 @@ struct PassCtx {
     DevBuf<uint32_t> rid[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
     DevBuf<uint8_t> bkt;
     DevBuf<float2> hits;
-    DevBuf<uint32_t> perm;            // trace-order permutation of the live slots (RT_COHERENT)
-    DevBuf<uint8_t> ckey;             // coherence key per slot, written by the reorder
     DevBuf<float> psum;               // this pass's per-pixel sums (when the caller gives no buffer)
     // pixel tiles with the reorder on: global slot per ray (ping-pong with the state), the global
     // bucket bytes (exchanged) and this owner's own bytes, their ranks, the global live count
@@ -1308,7 +1288,6 @@ struct rt_renderer {
     // shade/reorder (INLINE), saving the hit round trip and the trace launch per bounce.
     bool inline_hits = false;
     int fused_upto = -1;              // fused reorder at bounces <= this (when not `fused`)
-    bool coherent = RT_COHERENT != 0; // trace through a coherence-ordered permutation (RTAMD_COHERENT overrides)
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
     DevBuf<float4> spheres, tris, mats, nodes;
@@ -1386,8 +1365,6 @@ struct rt_renderer {
             fused_upto = -1;
             inline_hits = false;
         }
-        if (const char *f = std::getenv("RTAMD_COHERENT")) coherent = std::atoi(f) != 0;
-        if (tsort() || inline_hits) coherent = false;   // no trace kernel, or slots carried as data
         width = sc->width;
         height = sc->height;
         spp = sc->ray_count;
@@ -1488,8 +1465,7 @@ struct rt_renderer {
         const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
         // than half of the free device memory holds (1080p: ~2.9 GB per context).
-        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0) +
-                                                     (coherent ? 5 : 0)) +
+        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0)) +
                                  (size_t)trace_blocks_max * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
         size_t mem_free = 0, mem_total = 0;
         HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
@@ -1519,7 +1495,6 @@ struct rt_renderer {
             if ((rc = c.hits.alloc((size_t)max_rays))) return rc;
             if ((rc = c.overflow.alloc((size_t)trace_blocks_max * kBlock * 2 * (kStackMax - kStackLds)))) return rc;
             if ((rc = c.psum.alloc((size_t)pixels * 3))) return rc;
-            if (coherent && ((rc = c.perm.alloc((size_t)max_rays)) || (rc = c.ckey.alloc((size_t)max_rays)))) return rc;
             if (tsort()) {
                 for (int q = 0; q < 2; q++)
                     if ((rc = c.gslot[q].alloc((size_t)max_rays))) return rc;
@@ -1553,13 +1528,6 @@ struct rt_renderer {
         ds.inv_dim = v3(sc->inv_dimensions.x, sc->inv_dimensions.y, sc->inv_dimensions.z);
         ds.inv_w = sc->inv_width;
         ds.inv_h = sc->inv_height;
-        {   // coherence-key grid over the root box (trace order only; any box gives the same image)
-            const rt_bvh_node &r = sc->bvh[0];
-            auto sc4 = [](float lo, float hi) { return hi > lo ? 4.0f / (hi - lo) : 0.0f; };
-            ds.co_lo = v3(r.min_bound.x, r.min_bound.y, r.min_bound.z);
-            ds.co_scale = v3(sc4(r.min_bound.x, r.max_bound.x), sc4(r.min_bound.y, r.max_bound.y),
-                             sc4(r.min_bound.z, r.max_bound.z));
-        }
         HIPCHK(hipStreamSynchronize(s0));
         tm.mark("sync");
         tm.report();
@@ -1617,8 +1585,7 @@ struct rt_renderer {
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + 2 * b : nullptr, \
-                               (b > 0 && coherent) ? c.perm.p : nullptr);                                         \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + 2 * b : nullptr); \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
@@ -1665,8 +1632,7 @@ struct rt_renderer {
 #define RT_FSC2(SO, FI, IN)                                                                                      \
     hipLaunchKernelGGL((sort_scatter_shade_kernel<SO, FI, IN>), dim3(sort_grid), dim3(kBlock), 0, st, ds, pa,     \
                        c.bkt.p, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.hits.p, seed_term, lv, tiles,          \
-                       c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p,    \
-                       coherent ? c.ckey.p : nullptr)
+                       c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p)
 #define RT_FSC(SO, FI) do { if (inline_hits) RT_FSC2(SO, FI, true); else RT_FSC2(SO, FI, false); } while (0)
                     if (sort) {
                         if (b == 0) RT_FSC(true, 1); else RT_FSC(true, 0);
@@ -1675,29 +1641,18 @@ struct rt_renderer {
                     }
 #undef RT_FSC
 #undef RT_FSC2
-                } else {
-                    uint8_t *ck = coherent ? c.ckey.p : nullptr;
-                    if (b == 0 && tiled())
-                        hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                           c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                           c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, nullptr, nullptr,
-                                           nullptr, ck, ds.co_lo, ds.co_scale);
-                    else if (b == 0)
-                        hipLaunchKernelGGL(sort_scatter_kernel<1>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                           c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                           c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, nullptr, nullptr,
-                                           nullptr, ck, ds.co_lo, ds.co_scale);
-                    else
-                        hipLaunchKernelGGL(sort_scatter_kernel<0>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                           c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                           c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, nullptr, nullptr,
-                                           nullptr, ck, ds.co_lo, ds.co_scale);
-                }
-                if (coherent) {   // the next bounce's trace order
-                    const int wgrid = std::max(1, std::min((n + kCoWin - 1) / kCoWin, cus * 4));
-                    hipLaunchKernelGGL(window_perm_kernel, dim3(wgrid), dim3(kBlock), 0, st, c.ckey.p, c.live.p + b + 1,
-                                       c.perm.p);
-                }
+                } else if (b == 0 && tiled())
+                    hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
+                else if (b == 0)
+                    hipLaunchKernelGGL(sort_scatter_kernel<1>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
+                else
+                    hipLaunchKernelGGL(sort_scatter_kernel<0>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
+                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
                 HIPCHK(hipGetLastError());
                 if (pass_events) HIPCHK(hipEventRecord(s1, st));
                 cur = 1 - cur;
