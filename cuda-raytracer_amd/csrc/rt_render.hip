@@ -235,25 +235,10 @@ __device__ __forceinline__ void slab_pair(float4 a, float4 b, float4 c, V3 o, fl
 // of ~20 leaf lanes an early-out almost never skips work for all of them, so the nested branches
 // only cost their exec-mask bookkeeping (round 3, with the flat pop loop below: A/B teapot full
 // frame 6.94 -> 6.86 ms/pass over 5 rounds, 7.06 -> 6.86 over 3; 20 steps 7.24 -> 7.18, 7.27 -> 7.13).
-#ifndef RT_MT_RCP
-#define RT_MT_RCP 0
-#endif
-// 1/a bit-identical to the IEEE quotient: v_rcp_f32 and one FMA Newton step are correctly rounded for
-// every |a| in [2^-125, 2^125] on gfx950 (all 2^32 inputs checked, tools/experiments/rcp_check.hip);
-// a wave with a lane outside that range (zero, denormal, huge, inf, NaN) divides for those lanes.
-// 3 dependent VALU instead of the division's ~10.
-__device__ __forceinline__ float recip_exact(float a) {
-    const float r = __builtin_amdgcn_rcpf(a);
-    const float r1 = __builtin_fmaf(__builtin_fmaf(-a, r, 1.0f), r, r);
-    const float aa = __builtin_fabsf(a);
-    const bool ok = aa >= 0x1p-125f && aa <= 0x1p125f;
-    if (__builtin_expect(__ballot(!ok) != 0, 0)) return ok ? r1 : 1.0f / a;
-    return r1;
-}
 __device__ __forceinline__ bool ray_triangle_flat(V3 o, V3 d, V3 p1, V3 e1, V3 e2, float closest, float &t) {
     const V3 h = cross(d, e2);
     const float a = dot(h, e1);
-    const float f = RT_MT_RCP ? recip_exact(a) : 1 / a;
+    const float f = 1 / a;
     const V3 s = o - p1;
     const float u = dot(s, h) * f;
     const V3 q = cross(s, e1);
@@ -292,9 +277,6 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #endif
 #ifndef RT_SORT_GRID
 #define RT_SORT_GRID 0                // cap on the reorder's hist/scatter grid (0: 8 blocks per CU)
-#endif
-#ifndef RT_PRED_STEP
-#define RT_PRED_STEP 0                // 1: leaf and node bodies as one predicated block; 2: only in mixed waves
 #endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8)))
 template <bool SORTED, bool COUNT, int FIRST>
@@ -442,61 +424,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         const float4 *rec = in_leaf ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4;
         const float4 a = rec[0], b = rec[1], c = rec[2];
         const uint2 kids = *reinterpret_cast<const uint2 *>(rec + 3);   // node lanes only use it
-#if RT_PRED_STEP
-        // Both interpretations of the record for every lane, merged with selects: a wave whose lanes
-        // are partly at leaves and partly at internal nodes (nearly every wave of an incoherent
-        // bounce) ran the two bodies one after the other under exec masks; as one basic block their
-        // two dependency chains (the Möller–Trumbore division, the slab min/max tree) interleave.
-        if (RT_PRED_STEP == 1 || (__ballot(in_leaf) != 0 && __ballot(!in_leaf) != 0)) {
-            float t;
-            const bool thit =
-                ray_triangle_flat(o, d, v3(a.x, a.y, a.z), v3(a.w, b.x, b.y), v3(b.z, b.w, c.x), closest, t);
-            float t0, t1;
-            bool h0, h1;
-            slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
-            if (__builtin_expect(wave_nonfinite, 0)) {
-                float u0, u1;
-                const bool g0 = slab(a.x, a.z, b.x, b.z, c.x, c.z, o, ix, iy, iz, closest, u0);
-                const bool g1 = slab(a.y, a.w, b.y, b.w, c.y, c.w, o, ix, iy, iz, closest, u1);
-                if (!finite_inv) { h0 = g0; h1 = g1; t0 = u0; t1 = u1; }
-            }
-            const bool both = h0 && h1, any = h0 || h1;
-            const bool sel1 = h1 && (!h0 || t0 < t1);
-            const uint32_t next_ref = sel1 ? kids.y : kids.x, near_ref = sel1 ? kids.x : kids.y;
-            const float next_t = sel1 ? t1 : t0, near_t = sel1 ? t0 : t1;
-            // every lane writes the entry above its top (a leaf lane's sp does not move, so its write
-            // is overwritten before it is ever read); only a node lane with two hits pushes
-            col[min(sp, kStackLds) * kBlock] = make_uint2(near_ref, __float_as_uint(near_t));
-            const bool push = !in_leaf && both;
-            if (__builtin_expect(push && sp >= kStackLds, 0)) {
-                overflow[(sp - kStackLds) * lanes + gl] = near_ref;
-                overflow[dist_half + (sp - kStackLds) * lanes + gl] = __float_as_uint(near_t);
-            }
-            if (COUNT) {
-                tt += in_leaf ? 1u : 0u;
-                iv += in_leaf ? 0u : 1u;
-            }
-            const bool lhit = in_leaf && thit;    // leaf lanes: the triangle's outcome
-            closest = lhit ? t : closest;
-            index = lhit ? S.sphere_count + ti : index;
-            sp += push ? 1 : 0;                   // node lanes: the next child
-            const uint32_t nref = any ? next_ref : ref;
-            const bool descend = !in_leaf && any && !(next_t >= closest);
-            ref = in_leaf ? ref : nref;
-            if (COUNT) pn += descend ? 1u : 0u;
-            const bool dleaf = descend && (nref & kLeaf);
-            int nti = in_leaf ? ti + 1 : ti, nte = te;
-            if (__builtin_expect(dleaf && (nref & kBigLeaf), 0)) {
-                leaf_range(S, nref, nti, nte);
-            } else {
-                nti = dleaf ? (int)(nref & 0xFFFFFFu) : nti;
-                nte = dleaf ? nti + (int)((nref >> 24) & 0x3Fu) : nte;
-            }
-            need = in_leaf ? nti == te : (!descend || (dleaf && nti == nte));
-            ti = nti;
-            te = nte;
-        } else
-#endif
         if (in_leaf) {
             const float4 q0 = a, q1 = b;
             const float q2 = c.x;
