@@ -76,8 +76,32 @@ constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138
 #ifndef RT_SHADE_BPC
 #define RT_SHADE_BPC 8
 #endif
-constexpr int kSortItems = RT_SORT_ITEMS;   // sort tile = kBlock * kSortItems slots
+constexpr int kSortItems = RT_SORT_ITEMS;   // sort tile = kBlock * kSortItems slots (at most)
 constexpr int kSortTile = kBlock * kSortItems;
+// A reorder launch cuts the live prefix into tiles of 256-slot rounds, one workgroup per tile at a
+// time, the rounds of a tile in sequence (each waits for its slots' loads).  Big prefixes use
+// kSortItems rounds per tile; a small one (the tail bounces: 10^4-10^5 rays) uses fewer rounds and
+// more tiles, aiming at kTileTarget tiles, so its few workgroups do not each walk 16 dependent rounds
+// (round 3: a tail bounce's histogram and scatter took 40-60 us for ~20 k rays).  Every kernel of one
+// reorder derives the same rounds from the same live count.
+constexpr int kTileTarget = 2048;
+__host__ __device__ __forceinline__ int tile_rounds(int n) {
+    const int r = (int)(((int64_t)n + (int64_t)kBlock * kTileTarget - 1) / ((int64_t)kBlock * kTileTarget));
+    return r < 1 ? 1 : (r > kSortItems ? kSortItems : r);
+}
+__host__ __device__ __forceinline__ int tiles_of(int n) {
+    const int span = kBlock * tile_rounds(n);
+    return (n + span - 1) / span;
+}
+// the most tiles any live count up to n_max is cut into (a launch's grid)
+inline int max_tiles(int64_t n_max) {
+    return n_max >= (int64_t)kTileTarget * kSortTile ? (int)((n_max + kSortTile - 1) / kSortTile)
+                                                    : (int)std::min<int64_t>(kTileTarget, (n_max + kBlock - 1) / kBlock);
+}
+// counts/offsets stride (tiles) that covers every live count up to n_max
+inline int tile_stride(int64_t n_max) {
+    return (int)std::max<int64_t>(kTileTarget, (n_max + kSortTile - 1) / kSortTile);
+}
 constexpr int kBuckets = 65;
 constexpr int kCtrSlots = 64;       // striped copies of the work counters
 constexpr int kChunkMax = RT_CHUNK_MAX; // slots a wave takes from the trace queue per atomic...
@@ -715,21 +739,29 @@ __global__ __launch_bounds__(kBlock) void sort_hist_kernel(const uint8_t *__rest
                                                            const uint32_t *__restrict__ live_count, int tiles,
                                                            uint32_t *__restrict__ counts) {
     const int n = (int)*live_count;
+    const int R = tile_rounds(n), span = kBlock * R;
     __shared__ uint32_t h[kBuckets];
     // tile-stride: the grid is capped (the live prefix shrinks bounce by bounce; a block per
     // possible tile would dispatch thousands of empty workgroups in the tail bounces)
-    for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {
+    for (int tile = blockIdx.x; tile * span < n; tile += gridDim.x) {
         for (int b = threadIdx.x; b < kBuckets; b += kBlock) h[b] = 0;
         __syncthreads();
-        const int base = tile * kSortTile;
-#pragma unroll 4
-        for (int r = 0; r < kSortItems; r++) {
-            if (base + r * kBlock >= n) break;   // block-uniform: the live prefix's last tile is short
-            const int item = base + r * kBlock + threadIdx.x;
-            const bool valid = item < n;
-            const uint32_t b = valid ? bkt[item] : 0u;
-            const unsigned long long peers = match_bucket(b, valid);
-            if (valid && rank_below(peers) == 0) atomicAdd(&h[b], (uint32_t)__popcll(peers));
+        const int base = tile * span;
+        const int rounds = min(R, (n - base + kBlock - 1) / kBlock);   // block-uniform: the last tile is short
+        for (int r0 = 0; r0 < rounds; r0 += 4) {   // four rounds' loads in flight, then their ranking
+            uint32_t bv[4];
+            bool vv[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int item = base + (r0 + k) * kBlock + threadIdx.x;
+                vv[k] = r0 + k < rounds && item < n;
+                bv[k] = vv[k] ? bkt[item] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const unsigned long long peers = match_bucket(bv[k], vv[k]);
+                if (vv[k] && rank_below(peers) == 0) atomicAdd(&h[bv[k]], (uint32_t)__popcll(peers));
+            }
         }
         __syncthreads();
         for (int b = threadIdx.x; b < kBuckets; b += kBlock) counts[(size_t)b * tiles + tile] = h[b];
@@ -743,8 +775,7 @@ __global__ __launch_bounds__(kBlock) void sort_scan_kernel(const uint32_t *__res
                                                            uint32_t *__restrict__ offsets, uint32_t *__restrict__ totals,
                                                            uint32_t *__restrict__ live_next) {
     const uint32_t n = *live_count;
-    const int tiles = (int)((n + kSortTile - 1) / kSortTile);
-    (void)tiles_max;
+    const int tiles = tiles_of((int)n);
     __shared__ uint32_t wsum[kBlock / 64];
     __shared__ uint32_t carry;
     const int b = blockIdx.x;
@@ -799,13 +830,14 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
     const int n = (int)*live_count;
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
-    for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {   // tile-stride (capped grid)
+    const int R = tile_rounds(n), span = kBlock * R;
+    for (int tile = blockIdx.x; tile * span < n; tile += gridDim.x) {   // tile-stride (capped grid)
     bucket_runs(run, offsets, totals, tiles, tile);
     for (int k = threadIdx.x; k < (kBlock / 64) * kBuckets; k += kBlock) (&wcount[0][0])[k] = 0;
     __syncthreads();
     const int wave = threadIdx.x >> 6;
-    const int base = tile * kSortTile;
-    const int rounds = min(kSortItems, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
+    const int base = tile * span;
+    const int rounds = min(R, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
     for (int r = 0; r < rounds; r++) {
         const int item = base + r * kBlock + threadIdx.x;
         const bool valid = item < n;
@@ -882,22 +914,30 @@ __global__ __launch_bounds__(kBlock) void gsort_hist_kernel(const uint8_t *__res
                                                             const uint32_t *__restrict__ live_count, int tiles,
                                                             uint32_t *__restrict__ counts, uint32_t *__restrict__ bad) {
     const int n = (int)*live_count;
+    const int R = tile_rounds(n), span = kBlock * R;
     __shared__ uint32_t h[kBuckets];
     uint32_t nbad = 0;
-    for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {
+    for (int tile = blockIdx.x; tile * span < n; tile += gridDim.x) {
         for (int b = threadIdx.x; b < kBuckets; b += kBlock) h[b] = 0;
         __syncthreads();
-        const int base = tile * kSortTile;
-#pragma unroll 4
-        for (int r = 0; r < kSortItems; r++) {
-            if (base + r * kBlock >= n) break;
-            const int item = base + r * kBlock + threadIdx.x;
-            const bool valid = item < n;
-            const uint32_t v = valid ? g[item] : 1u;
-            const uint32_t b = exchanged_bucket(v);
-            nbad += (valid && !(v >= 1 && v <= kBuckets)) ? 1u : 0u;
-            const unsigned long long peers = match_bucket(b, valid);
-            if (valid && rank_below(peers) == 0) atomicAdd(&h[b], (uint32_t)__popcll(peers));
+        const int base = tile * span;
+        const int rounds = min(R, (n - base + kBlock - 1) / kBlock);
+        for (int r0 = 0; r0 < rounds; r0 += 4) {   // four rounds' loads in flight, then their ranking
+            uint32_t vr[4];
+            bool vv[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int item = base + (r0 + k) * kBlock + threadIdx.x;
+                vv[k] = r0 + k < rounds && item < n;
+                vr[k] = vv[k] ? g[item] : 1u;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t b = exchanged_bucket(vr[k]);
+                nbad += (vv[k] && !(vr[k] >= 1 && vr[k] <= kBuckets)) ? 1u : 0u;
+                const unsigned long long peers = match_bucket(b, vv[k]);
+                if (vv[k] && rank_below(peers) == 0) atomicAdd(&h[b], (uint32_t)__popcll(peers));
+            }
         }
         __syncthreads();
         for (int b = threadIdx.x; b < kBuckets; b += kBlock) counts[(size_t)b * tiles + tile] = h[b];
@@ -918,13 +958,14 @@ __global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__rest
     const int n = (int)*live_count;
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
-    for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {
+    const int R = tile_rounds(n), span = kBlock * R;
+    for (int tile = blockIdx.x; tile * span < n; tile += gridDim.x) {
         bucket_runs(run, offsets, totals, tiles, tile);
         for (int k = threadIdx.x; k < (kBlock / 64) * kBuckets; k += kBlock) (&wcount[0][0])[k] = 0;
         __syncthreads();
         const int wave = threadIdx.x >> 6;
-        const int base = tile * kSortTile;
-        const int rounds = min(kSortItems, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
+        const int base = tile * span;
+        const int rounds = min(R, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
         for (int r = 0; r < rounds; r++) {
             const int item = base + r * kBlock + threadIdx.x;
             const bool valid = item < n;
@@ -973,13 +1014,14 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
     const int n = (int)*live_count;
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
-    for (int tile = blockIdx.x; tile * kSortTile < n; tile += gridDim.x) {
+    const int R = tile_rounds(n), span = kBlock * R;
+    for (int tile = blockIdx.x; tile * span < n; tile += gridDim.x) {
         bucket_runs(run, offsets, totals, tiles, tile);
         for (int k = threadIdx.x; k < (kBlock / 64) * kBuckets; k += kBlock) (&wcount[0][0])[k] = 0;
         __syncthreads();
         const int wave = threadIdx.x >> 6;
-        const int base = tile * kSortTile;
-        const int rounds = min(kSortItems, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
+        const int base = tile * span;
+        const int rounds = min(R, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
         for (int r = 0; r < rounds; r++) {
             const int item = base + r * kBlock + threadIdx.x;
             const bool valid = item < n;
@@ -1087,6 +1129,19 @@ __global__ __launch_bounds__(kBlock) void box_blur_kernel(const float *__restric
 __global__ __launch_bounds__(kBlock) void add_kernel(float *__restrict__ img, const float *__restrict__ add, int n) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i < n) img[i] = img[i] + add[i];
+}
+// The same add four floats per lane (both buffers 16-B aligned; the host checks): one pass's add into
+// the framebuffer is on the pass-order chain of every frame.
+__global__ __launch_bounds__(kBlock) void add4_kernel(float *__restrict__ img, const float *__restrict__ add, int n) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    const int n4 = n >> 2;
+    if (i < n4) {
+        float4 a = reinterpret_cast<float4 *>(img)[i];
+        const float4 b = reinterpret_cast<const float4 *>(add)[i];
+        a.x = a.x + b.x; a.y = a.y + b.y; a.z = a.z + b.z; a.w = a.w + b.w;
+        reinterpret_cast<float4 *>(img)[i] = a;
+    }
+    if (i < (n & 3)) img[(n4 << 2) + i] = img[(n4 << 2) + i] + add[(n4 << 2) + i];
 }
 
 // ==================================================================== host side
@@ -1389,7 +1444,7 @@ struct rt_renderer {
         tm.mark("occupancy query");
         trace_blocks_max = std::max(1, cus * std::max(1, per_cu));
         trace_blocks = trace_blocks_max;
-        const int tiles = (int)((max_rays + kSortTile - 1) / kSortTile);
+        const int tiles = tile_stride(max_rays);
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
         // than half of the free device memory holds (1080p: ~2.9 GB per context).
         const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0)) +
@@ -1472,12 +1527,12 @@ struct rt_renderer {
         const int64_t tpix = tile_pixels();     // pixels this render casts rays for
         const int n = (int)(rtc * tpix);
         const int grid = blocks_for(n);
-        const int tiles = (n + kSortTile - 1) / kSortTile;
+        const int tiles = tile_stride(n);     // counts stride; a launch's tiles follow its live count
         const int tgrid = std::min(grid, trace_blocks);
         const int sgrid = std::min(grid, cus * RT_SHADE_BPC);
         // tile-stride reorder kernels on at most 8 blocks per CU: in the tail bounces a block per
         // possible tile dispatched ~10^4 empty workgroups per launch (A/B: +0.3-0.5 %)
-        const int sort_grid = std::min(tiles, RT_SORT_GRID > 0 ? RT_SORT_GRID : cus * 8);
+        const int sort_grid = std::max(1, std::min(max_tiles(n), RT_SORT_GRID > 0 ? RT_SORT_GRID : cus * 8));
         hipStream_t st = c.stream;
         int cur = 0;
         if (n == 0) {                           // a tile owner with no stripe of this image
@@ -1638,7 +1693,7 @@ struct rt_renderer {
         c.t_n = (int)(c.t_rtc * tile_pixels());
         c.t_cur = 0;
         c.t_lg = (uint64_t)c.t_rtc * width * height;   // every generated ray is live at bounce 0
-        c.t_tiles_g = (int)((c.t_lg + kSortTile - 1) / kSortTile);
+        c.t_tiles_g = tile_stride((int64_t)c.t_lg);
         hipLaunchKernelGGL(fill_live_kernel, dim3(1), dim3(256), 0, c.stream, c.live.p, (uint32_t)c.t_n, bounces + 1,
                            c.queue.p, nullptr);
         hipLaunchKernelGGL(set_count_kernel, dim3(1), dim3(64), 0, c.stream, c.glive.p, (uint32_t)c.t_lg, nullptr);
@@ -1726,7 +1781,7 @@ struct rt_renderer {
             if (rc) return rtamd::fail(RT_E_INVALID, "tile exchange callback failed (" + std::to_string(rc) + ")");
         }
         const int tg = c.t_tiles_g;
-        const int ggrid = std::max(1, std::min((int)((lg + kSortTile - 1) / kSortTile), cus * 8));
+        const int ggrid = std::max(1, std::min(max_tiles((int64_t)lg), cus * 8));
         // global: buckets of every live slot -> new global slots of this owner's slots (newpos) and
         // the next global live count
         hipLaunchKernelGGL(gsort_hist_kernel, dim3(ggrid), dim3(kBlock), 0, st, c.gbytes.p, c.glive.p, tg,
@@ -1741,8 +1796,8 @@ struct rt_renderer {
         // local: this owner's rays in the same stable order (local order = ascending global slot),
         // each carrying its new global slot
         const uint32_t *lv = c.live.p + b;
-        const int tiles = (c.t_n + kSortTile - 1) / kSortTile;
-        const int sort_grid = std::max(1, std::min(tiles, RT_SORT_GRID > 0 ? RT_SORT_GRID : cus * 8));
+        const int tiles = tile_stride(c.t_n);
+        const int sort_grid = std::max(1, std::min(max_tiles(c.t_n), RT_SORT_GRID > 0 ? RT_SORT_GRID : cus * 8));
         const int cur = c.t_cur;
         hipLaunchKernelGGL(sort_hist_kernel, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, lv, tiles, c.sort_counts.p);
         hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, lv, tiles,
@@ -1858,7 +1913,11 @@ struct rt_renderer {
         hipEvent_t prev_fb = nullptr;
         auto add_pass = [&](PassCtx &c, int p, float *sums) -> int {
             if (prev_fb) HIPCHK(hipStreamWaitEvent(c.stream, prev_fb, 0));
-            hipLaunchKernelGGL(add_kernel, dim3(blocks_for(px3)), dim3(kBlock), 0, c.stream, fb.p, sums, (int)px3);
+            if ((reinterpret_cast<uintptr_t>(sums) & 15) == 0)
+                hipLaunchKernelGGL(add4_kernel, dim3(blocks_for(std::max<int64_t>(px3 / 4, 4))), dim3(kBlock), 0, c.stream,
+                                   fb.p, sums, (int)px3);
+            else
+                hipLaunchKernelGGL(add_kernel, dim3(blocks_for(px3)), dim3(kBlock), 0, c.stream, fb.p, sums, (int)px3);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c.fb_done, c.stream));
             prev_fb = c.fb_done;

@@ -47,3 +47,23 @@ def test_bench_line_fractions_at_most_one():
     assert 0 < roof["frac"] <= 1 and 0 < roof["traffic_frac"] <= 1
     assert 0 < roof["l2"]["frac"] <= 1 and 0 < roof["frame"]["frac"] <= 1
     assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
+
+
+def test_roofline_restated_on_exclusive_launches():
+    """bench.roofline (round 3): achieved = algorithmic bytes (scene once per XCD) / the exclusive launch
+    duration; traffic_frac = the PMC bytes over the same duration; the shared-chip spans only in `shared`."""
+    bench = _bench()
+    counted = {"live_segments": 79_000_000, "generated_rays": 41_472_000, "nodes_popped": 800_000_000,
+               "internal_visits": 680_000_000, "triangle_tests": 300_000_000}
+    excl = {"launches": 16, "ms_per_launch": 0.7, "trace_ms": 11.2, "kernel_ms": 15.0, "counted": counted}
+    scene_bytes = 32 * 252_099 + 48 * 126_050
+    roof = bench.roofline(excl, counted, 16, 2.3, scene_bytes, 0, WORKLOAD, 0.14, 20)
+    comp = (24 * (79_000_000 - 41_472_000) + 8 * 79_000_000 + 16 * 8 * scene_bytes) / 16
+    assert roof["bytes_per_launch"] == int(comp)
+    assert abs(roof["achieved"] - comp / 0.7e-3 / 1e9) < 0.1
+    assert abs(roof["frac"] - roof["achieved"] / 8000.0) < 1e-4
+    assert roof["shared"]["ms_per_launch"] == 2.3 and roof["ms_per_launch"] == 0.7
+    pmc = bench.load_pmc(WORKLOAD)
+    if pmc:
+        assert abs(roof["traffic_frac"] - pmc["trace_bytes_per_launch"] / 0.7e-3 / 1e9 / 8000.0) < 1e-3
+    assert roof["logical_per_step"]["achieved"] > 0
