@@ -226,12 +226,13 @@ def roofline(excl, counted, launches, trace_ms, scene_bytes, spheres, workload, 
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": "trace_kernel (BVH traversal + Moller-Trumbore + slab + sphere loop), per launch",
             "bytes_per_launch": int(comp_ex), "ms_per_launch": round(ms_ex, 4), "launches": n_ex,
+            "exclusive_pass_kernel_ms": round(excl["kernel_ms"], 3),
             "achieved_def": "algorithmic HBM bytes per trace launch of pass 0 run alone on the chip (24 B ray read "
                             "per live segment past bounce 0 + 8 B hit write per live segment + the scene's node and "
                             "triangle arrays (reference layouts, 32 / 48 B) once per XCD: 8 non-coherent 4 MB L2s each "
                             "fetch the scene) / its exclusive average launch duration (device wall clock, first wave "
                             "start to last wave end, one pass context, trace grid = every resident workgroup, best "
-                            "of 3; bench.py exclusive_pass)",
+                            "of 3, measured before the warmup; bench.py exclusive_pass)",
             "traffic_def": None if not pmc else
             "measured fabric-side bytes per trace launch, rocprofv3 --pmc over exactly pass 0 with dispatches "
             "serialised (%s; reads priced by request size TCC_EA0_RDREQ_{128B,64B,32B}, = 2 x FETCH_SIZE for 128-B "
@@ -441,6 +442,11 @@ def main():
     # No per-bounce HIP events in the timed steps (five marker packets per bounce in every pass's
     # stream cost ~2 %); the per-launch kernel times come from an untimed re-run below.
     ren.set_event_timing(False)
+    # the dominant kernel's exclusive launch durations (roofline), before the warmup: measured in the
+    # same state as the one-pass PMC run they are compared with, not after minutes of full load
+    excl = None
+    if not args.no_extras and not args.no_counters and not tiles and rank == 0:
+        excl = exclusive_pass(scene, sort, local)
     warm = {}
     run_steps(args.warmup, warm)
     barrier_sync()
@@ -451,7 +457,7 @@ def main():
     elapsed = time.perf_counter() - t0
 
     # ---- untimed legs (every rank takes part: they contain collectives)
-    evrun, counted, frame_s, parity, excl = {}, None, None, None, None
+    evrun, counted, frame_s, parity = {}, None, None, None
     if not args.no_extras:
         # per-launch kernel times: the same steps again with per-bounce HIP events on each pass's stream
         ren.set_event_timing(True)
@@ -490,8 +496,6 @@ def main():
                       if gold else "no golden hash for this workload",
                       "reference_rms": "parity unpinned: the reference's GPU path cannot run here (SURVEY.md §8c), "
                                        "the oracle is a cited restatement; image error vs the reference is not measured"}
-        if not tiles and rank == 0 and not args.no_counters:
-            excl = exclusive_pass(scene, sort, local)
     elapsed, frame_s_max = reduce([elapsed, frame_s or 0.0], "max")
     # ranks that took part, as the collective backend counts them (a SCALE run can be checked for
     # RCCL seeing N ranks): an all-reduce of 1 per rank

@@ -118,6 +118,12 @@ constexpr int kTraceOccPct = RT_TRACE_OCC;
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
 constexpr int kQueueStride = 64;     // words between shards (256 B: one shard per cache line)
 constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFFFFF)
+// Per-launch span words (rt_renderer_set_event_timing): 8 start slots then 8 end slots, one per XCD
+// (workgroup i runs on XCD i % 8), each written by one atomic per workgroup -- one word for a whole
+// 8192-wave launch serialised its waves' atomics and lengthened the span it measured (round 3:
+// 0.82 vs the profiler's 0.66 ms per exclusive teapot launch).
+constexpr int kSpanSlots = 8;
+constexpr int kSpanWords = 2 * kSpanSlots;
 constexpr uint32_t kLeaf = 0x80000000u, kBigLeaf = 0x40000000u;
 
 struct DevScene {
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
     // before its first wave and the stream's marker packets (what rocprofv3 reports)
-    if (tspan && lane_id() == 0) atomicMin(&tspan[0], (unsigned long long)wall_clock64());
+    if (tspan && threadIdx.x == 0) atomicMin(&tspan[blockIdx.x % kSpanSlots], (unsigned long long)wall_clock64());
     uint2 *col = stack + threadIdx.x;
     // Overflow tail of the stack (entries >= kStackLds, rare) in a global per-lane buffer,
     // [entry][lane] for coalescing; refs and distances in two 32-bit halves so the compiler cannot
@@ -549,7 +555,10 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         }
     }
     if (lane_id() == 0 && nl) atomicAdd(&cs->live, nl);
-    if (tspan && lane_id() == 0) atomicMax(&tspan[1], (unsigned long long)wall_clock64());
+    if (tspan) {                        // the workgroup's last wave: one atomic per workgroup
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(&tspan[kSpanSlots + blockIdx.x % kSpanSlots], (unsigned long long)wall_clock64());
+    }
 #ifdef RT_PROFILE
     prof[11] = wave_sum((unsigned)prof[10]);   // pop iterations summed over the lanes
     if (lane_id() == 0)
@@ -697,7 +706,7 @@ __global__ void fill_live_kernel(uint32_t *__restrict__ live, uint32_t n, int co
     if (i < count) live[i] = n;
     for (int k = i; k < count * kQueues * kQueueStride; k += blockDim.x) queue[k] = 0;
     if (tspan)
-        for (int k = i; k < 2 * count; k += blockDim.x) tspan[k] = (k & 1) ? 0ull : ~0ull;
+        for (int k = i; k < kSpanWords * count; k += blockDim.x) tspan[k] = (k % kSpanWords) >= kSpanSlots ? 0ull : ~0ull;
 }
 
 
@@ -1458,6 +1467,11 @@ struct rt_renderer {
         if (pass_hint > 0) cap = std::min<size_t>(cap, (size_t)pass_hint);   // a one-shot render of fewer passes
         nctx = !passes ? 0 : (int)std::min<size_t>({cap, (size_t)std::max(1, pass_count()),
                                                     std::max<size_t>(1, mem_free / 2 / ctx_bytes)});
+        // Pixel tiles with the reorder on: the exchange order follows the passes in flight, which
+        // must therefore be the same on every owner; it may not depend on this device's free memory.
+        if (passes && tsort() && (size_t)nctx < std::min<size_t>(cap, (size_t)std::max(1, pass_count())))
+            return rtamd::fail(RT_E_OOM, "pixel tiles with sort on: device memory holds only " + std::to_string(nctx) +
+                                             " passes in flight; set RTAMD_INFLIGHT to the same lower value on every owner");
         const int inflight = nctx;
         for (int k = 0; k < inflight; k++) {
             PassCtx &c = ctx[k];
@@ -1518,7 +1532,7 @@ struct rt_renderer {
 
     // Pass p of `while (remaining_rays)` (raytracing.cu:222-254) on context c; the pass's
     // per-pixel sums go to `sums` (W*H*3).
-    // tspan: 2 * (bounces + 1) words for this pass's trace-launch wall-clock spans, or null
+    // tspan: kSpanWords * (bounces + 1) words for this pass's trace-launch wall-clock spans, or null
     int enqueue_pass(PassCtx &c, int p, float *sums, int64_t &sorted, unsigned long long *tspan) {
         const int before = spp - 20 * p;
         const int rtc = std::min(before, 20);
@@ -1567,7 +1581,7 @@ struct rt_renderer {
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + 2 * b : nullptr); \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr); \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
@@ -1900,8 +1914,8 @@ struct rt_renderer {
             trace_blocks = std::max(1, trace_blocks_max * pct / 100);
         }
         hipStream_t s0 = stream();
-        if (pass_events && tspans.n < (size_t)std::max(count, 1) * 2 * (bounces + 1)) {
-            if (int rc = tspans.alloc((size_t)std::max(count, 1) * 2 * (bounces + 1))) return rc;
+        if (pass_events && tspans.n < (size_t)std::max(count, 1) * kSpanWords * (bounces + 1)) {
+            if (int rc = tspans.alloc((size_t)std::max(count, 1) * kSpanWords * (bounces + 1))) return rc;
             if (!wall_khz) HIPCHK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, device));
         }
         HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, s0));
@@ -1984,7 +1998,7 @@ struct rt_renderer {
                 const int p = pass_begin + k * stride;
                 float *sums = sums_of(c, k);
                 const int rc = enqueue_pass(c, p, sums, sorted,
-                                            pass_events ? tspans.p + (size_t)k * 2 * (bounces + 1) : nullptr);
+                                            pass_events ? tspans.p + (size_t)k * kSpanWords * (bounces + 1) : nullptr);
                 if (rc) return rc;
                 if (int rc2 = add_pass(c, p, sums)) return rc2;
             }
@@ -2050,12 +2064,16 @@ struct rt_renderer {
             // trace launches: the device wall-clock span from the first wave's start to the last
             // wave's end (the stream's events would add the queueing before the first wave)
             if (pass_events && !inline_hits && !tsort() && count > 0) {
-                std::vector<unsigned long long> sp((size_t)count * 2 * (bounces + 1));
+                std::vector<unsigned long long> sp((size_t)count * kSpanWords * (bounces + 1));
                 HIPCHK(hipMemcpy(sp.data(), tspans.p, sp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
                 for (int k = 0; k < count; k++)
                     for (int b = 0; b < bounces; b++) {
-                        const unsigned long long t0 = sp[((size_t)k * (bounces + 1) + b) * 2];
-                        const unsigned long long t1 = sp[((size_t)k * (bounces + 1) + b) * 2 + 1];
+                        const unsigned long long *w = &sp[((size_t)k * (bounces + 1) + b) * kSpanWords];
+                        unsigned long long t0 = ~0ull, t1 = 0;
+                        for (int x = 0; x < kSpanSlots; x++) {
+                            t0 = std::min(t0, w[x]);
+                            t1 = std::max(t1, w[kSpanSlots + x]);
+                        }
                         if (t1 >= t0 && t0 != ~0ull) {
                             trc += (double)(t1 - t0) / wall_khz;
                             trace_launches++;

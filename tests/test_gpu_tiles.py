@@ -185,3 +185,24 @@ def test_multi_device_failure_after_setup_returns(gpu, monkeypatch, shard_tiles)
     fb, _ = R.render(psc, sort=True, devices=[0], shard_tiles=shard_tiles)   # the library still works
     ref, _ = O.OracleScene("%s/cornell.scene" % R.ASSETS, image=(32, 32, 8, 2)).render(sort=True)
     assert np.array_equal(fb, ref)
+
+
+@pytest.mark.parametrize("scene,image", [("teapot", (40, 24, 45, 8)), ("lamp_available", (32, 18, 20, 32))])
+def test_rccl_exchange_one_rank(gpu, scene, image):
+    """rt_rccl_unique_id + rt_renderer_set_exchange_rccl with sort on: owner 0 of a 2-owner split whose
+    stripes cover the whole image (one stripe of H rows; owner 1 has none) joins a one-rank RCCL
+    communicator, so every per-bounce exchange runs the library's in-place ncclAllReduce on the pass
+    stream (an identity sum at one rank) and the render equals the oracle's bit for bit.  RCCL refuses
+    two ranks on one GPU, so this is the RCCL exchange's reach on a one-GPU box."""
+    path = "%s/%s.scene" % (R.ASSETS, scene)
+    W, H = image[0], image[1]
+    ref, rst = O.OracleScene(path, image=image).render(sort=True)
+    uid = R.rccl_unique_id()
+    assert len(uid) == R.RCCL_ID_BYTES
+    r = R.Renderer(R.Scene(path, image=image), sort=True, tiles=(2, 0, H))
+    r.set_exchange_rccl(uid, 1, 0)
+    st = r.run(pass_begin=0, count=-1)
+    fb = r.framebuffer()
+    r.close()
+    assert np.array_equal(fb, ref)
+    assert st["live_segments"] == rst["live_segments"]
