@@ -132,7 +132,6 @@ struct DevScene {
     const uint16_t *mat_idx;
     const float4 *mats;               // 3 x float4: diffuse,metal | specular,rough | emit,ior
     const float4 *nodes;              // 4 x float4 per internal node (child-pair record)
-    uint32_t tri_off;                 // byte offset of tris from nodes (one allocation, < 4 GB)
     const int2 *big_leaves;           // {begin, end} for leaves that do not fit a ref
     const float *env;                 // env_h * env_w * 3
     int sphere_count, env_w, env_h, width, height;
@@ -145,9 +144,6 @@ struct DevScene {
 #ifdef RT_PROFILE
 // Wave-level traversal profile (debug builds only): see tools/variants.sh + RT_PROFILE=1.
 __device__ unsigned long long g_prof[2][12];   // [bounce 0, later bounces]
-__device__ unsigned long long g_fprof[2][8];   // trace_free_kernel: [bounce 0, later][see trace_free_kernel]
-__device__ unsigned int g_fdbg_n;
-__device__ float g_fdbg[16][12];                // rays past 20000 iterations: o, d, c0m, best, second, iters, ex, sp, ...
 #define PROF(i, v) (prof[i] += (v))
 #else
 #define PROF(i, v) ((void)0)
@@ -155,7 +151,6 @@ __device__ float g_fdbg[16][12];                // rays past 20000 iterations: o
 
 struct Counters {                     // device-side work counters (u64, one atomic per wave)
     unsigned long long live, pn, iv, tt, st, hits, misses, hits_sphere;
-    unsigned long long redo[4];       // re-traced rays by cause: 1/d or forced, tie or NaN t, stack, entry check
 };
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
@@ -307,12 +302,6 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #ifndef RT_TRACE_WPE
 #define RT_TRACE_WPE 8
 #endif
-#ifndef RT_SADDR
-#define RT_SADDR 0                    // record loads as one scalar base + 32-bit offset
-#endif
-#ifndef RT_UBIG
-#define RT_UBIG 0                     // leaf entry as selects, big-leaf range behind a wave-uniform branch
-#endif
 #ifndef RT_FUSED_MAX_TRIS
 #define RT_FUSED_MAX_TRIS 4096        // fused reorder for scenes up to this many triangles (see enqueue_pass)
 #endif
@@ -462,18 +451,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         // costs one memory round trip whatever mix of leaf and internal lanes the wave holds.
         bool need = false;              // the lane needs the next node from its stack
         const bool in_leaf = ti < te;
-#if RT_SADDR
-        // nodes and triangles share one allocation: a 32-bit byte offset from one uniform base, so
-        // the four record loads take the scalar-base + 32-bit-offset form (no 64-bit address math)
-        // ti * 48 as (3 ti) << 4 and ref * 64, both computed, then one select (no branch; the
-        // opaque 3 ti keeps the compiler from folding it back into a quarter-rate multiply)
-        uint32_t ti3 = ((uint32_t)ti << 1) + (uint32_t)ti, off_n = ref << 6;
-        asm volatile("" : "+v"(ti3), "+v"(off_n));
-        const uint32_t off = in_leaf ? S.tri_off + (ti3 << 4) : off_n;
-        const float4 *rec = reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(S.nodes) + off);
-#else
         const float4 *rec = in_leaf ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4;
-#endif
         const float4 a = rec[0], b = rec[1], c = rec[2];
         const uint2 kids = *reinterpret_cast<const uint2 *>(rec + 3);   // node lanes only use it
         if (in_leaf) {
@@ -520,17 +498,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             if (both) sp++;
             ref = any ? next_ref : ref;
             const bool descend = any && !(next_t >= closest);
-#if RT_UBIG
-            // entering a leaf as selects; only a big leaf's range load branches (wave-uniform, rare)
-            if (COUNT) pn += descend ? 1u : 0u;
-            const bool dleaf = descend && (ref & kLeaf);
-            ti = dleaf ? (int)(ref & 0xFFFFFFu) : ti;
-            te = dleaf ? ti + (int)((ref >> 24) & 0x3Fu) : te;
-            if (__builtin_expect(__ballot(dleaf && (ref & kBigLeaf)) != 0, 0)) {
-                if (dleaf && (ref & kBigLeaf)) leaf_range(S, ref, ti, te);
-            }
-            need = !descend || (dleaf && ti == te);
-#else
             need = !descend;
             if (descend) {
                 if (COUNT) pn++;
@@ -539,7 +506,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     need = ti == te;
                 }
             }
-#endif
         }
 #ifdef RT_PROFILE
         if (__ballot(need)) PROF(5, 1);
@@ -567,20 +533,12 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             ref = take ? e.x : ref;
             if (COUNT) pn += take ? 1u : 0u;
             const bool leaf = take && (ref & kLeaf);
-#if RT_UBIG
-            ti = leaf ? (int)(ref & 0xFFFFFFu) : ti;
-            te = leaf ? ti + (int)((ref >> 24) & 0x3Fu) : te;
-            if (__builtin_expect(__ballot(leaf && (ref & kBigLeaf)) != 0, 0)) {   // wave-uniform, rare
-                if (leaf && (ref & kBigLeaf)) leaf_range(S, ref, ti, te);
-            }
-#else
             if (__builtin_expect(leaf && (ref & kBigLeaf), 0)) {
                 leaf_range(S, ref, ti, te);
             } else {
                 ti = leaf ? (int)(ref & 0xFFFFFFu) : ti;
                 te = leaf ? ti + (int)((ref >> 24) & 0x3Fu) : te;
             }
-#endif
             need = !empty && (!take || (leaf && ti == te));
         }
     }
@@ -607,367 +565,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         for (int i = 0; i < 12; i++)
             if (i != 10) atomicAdd(&g_prof[FIRST ? 0 : 1][i], prof[i]);
 #endif
-}
-
-// ---------------------------------------------------------------- order-free traversal
-// The reference pushes the near child first and so visits the FAR child first (scene.cu:204-225):
-// by the time it pops a near subtree, its running closest rarely culls it.  Measured with the
-// oracle's own scenes (tools/experiments/exhaustive_probe.cpp, bounce-0 and diffuse bounce-1 rays),
-// testing EVERY slab-hit subtree, in any order, costs only 0.7-2.5 % more node visits and triangle
-// tests than the reference's traversal.  Its answer is then order-free, and it equals the
-// reference's whenever this holds (proof sketch; DESIGN.md §3 "Order-free traversal"):
-//   c0 = the closest after the sphere loop; S = the subtrees whose every path box passes the slab
-//   test bounded by c0 and has entry distance < c0 (the reference culls the others whatever it
-//   finds, its closest never exceeds c0); candidates = triangles of S's leaves accepted against c0.
-//   The reference tests a subset of the candidates, so its answer r >= t* = the candidates' least t.
-//   Let w be the unique candidate at t* and `second` the least t of the other candidates (c0 if
-//   none).  Until it tests w the reference's closest is >= second, and a box entry distance is
-//   monotone down the tree (child bounds lie inside the parent's; per-axis rounding is monotone), so
-//   if the entry distance of w's leaf is < second no box on w's path is culled, w is tested with
-//   closest > t* and accepted: r = t*, index w.
-// A ray starts over in the reference order, on the same lane, when that check fails, when another candidate ties t*, when a candidate's t is NaN (the reference accepts a NaN t
-// and then compares against a NaN closest), when 1/d has a non-finite component (the literal slab
-// fold) or when its stack outgrows kStackMax.  On the scenes of this repo that is ~0 rays.
-// What the freedom buys is SIMD efficiency: a lane that reaches a leaf keeps it pending and goes on
-// descending (Aila & Laine's speculative traversal), and each step runs ONE body for the whole wave
-// -- a triangle test for the lanes with a pending leaf, or a node test for the lanes with a node --
-// instead of both bodies in ~90 % of the reference-order kernel's steps (RT_PROFILE, teapot).
-#ifndef RT_FREE_MASKED
-#define RT_FREE_MASKED 0                // load each chain's record only on the lanes that use it
-#endif
-#ifndef RT_FREE_FILL
-#define RT_FREE_FILL 0                  // lanes with a node also pop a leaf into a free pending slot
-#endif
-#ifndef RT_FREE_WPE1
-#define RT_FREE_WPE1 8                  // waves per SIMD of the bounce-0 order-free kernels
-#endif
-template <int FIRST>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FIRST ? RT_FREE_WPE1 : RT_TRACE_WPE, 8)))
-void trace_free_kernel(
-    DevScene S, PassArgs pa, const float4 *__restrict__ geo, const uint32_t *__restrict__ live_count,
-    uint32_t *__restrict__ queue, float2 *__restrict__ hits, uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
-    unsigned long long *__restrict__ tspan, int force_exact) {
-    __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // {ref, entry distance}; + one scratch entry per lane
-    if (tspan && threadIdx.x == 0) atomicMin(&tspan[blockIdx.x % kSpanSlots], (unsigned long long)wall_clock64());
-    uint2 *col = stack + threadIdx.x;
-    const uint32_t lanes = gridDim.x * kBlock, gl = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t dist_half = lanes * (kStackMax - kStackLds);
-    const uint32_t L = __builtin_amdgcn_readfirstlane(*live_count);
-    const uint32_t waves = gridDim.x * (kBlock / 64);
-    const uint32_t chunk = min((uint32_t)kChunkMax, max((uint32_t)kChunkMin, (L / (4 * waves) + 63) & ~63u));
-    uint32_t shard = blockIdx.x % kQueues, tried = 0;
-    uint32_t q_next = 0, q_end = 0;
-    bool exhausted = false;
-    int slot = -1;                      // < 0: no ray; <= -2: done with slot -2 - slot, result not yet stored
-    V3 o{0, 0, 0}, d{0, 0, 0};
-    float ix = 0, iy = 0, iz = 0;
-    float c0m = 0;                      // the float below c0: n <= min(F, c0m) <=> n <= F && n < c0
-    float best = 0, second = 0, wn = 0; // least candidate t, least t of the others, winner's leaf entry
-    int index = -1;
-    uint32_t bad = 0;                   // the order-free answer cannot be proven: cause bits (Counters::redo)
-    bool ex = false;                    // the lane runs the reference-order traversal for its ray
-    bool has_node = false;              // ref: an internal node (child-pair record) still to test
-    uint32_t ref = 0;
-    int ti = 0, te = 0;                 // pending leaf [ti, te) while ti < te, entry distance ln
-    float ln = 0;
-    int sp = 0;
-    unsigned nlive = 0;
-    uint32_t redo[4] = {0, 0, 0, 0};    // wave totals by cause (wave-uniform)
-    // a ray's start, for both traversals: the sphere loop (scene.cu:338-372), then the root, popped at
-    // distance 0 < closest (scene.cu:142-155)
-    auto begin_ray = [&]() {
-        float c0 = 1e30f;
-        index = -1;
-        for (int i = 0; i < S.sphere_count; i++) {
-            const float4 sph = S.spheres[i];
-            float t;
-            if (ray_sphere(o, d, v3(sph.x, sph.y, sph.z), sph.w, c0, t)) { c0 = t; index = i; }
-        }
-        best = second = c0;
-        c0m = __int_as_float(__float_as_int(c0) - 1);   // c0 >= 0.005 > 0
-        wn = 0;
-        sp = 0;
-        ref = S.root_ref;
-        has_node = !(ref & kLeaf);
-        ti = te = 0;
-        ln = 0;
-        if (ref & kLeaf) leaf_range(S, ref, ti, te);
-    };
-#ifdef RT_PROFILE
-    unsigned long long fprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned iters = 0;
-#endif
-    while (true) {
-        unsigned long long idle = __ballot(slot < 0);
-        if (!exhausted && __popcll(idle) >= (FIRST ? kRefillFirst : kRefill)) {
-            if (slot <= -2) {
-                hits[-2 - slot] = make_float2(best, __int_as_float(index));
-                slot = -1;
-            }
-            bool fresh = false;
-            while (idle && !exhausted) {
-                if (q_next >= q_end) {
-                    const uint32_t seg_lo = (uint32_t)(((uint64_t)L * shard) / kQueues);
-                    const uint32_t seg_hi = (uint32_t)(((uint64_t)L * (shard + 1)) / kQueues);
-                    uint32_t c = 0;
-                    if (lane_id() == 0) c = atomicAdd(queue + shard * kQueueStride, chunk);
-                    c = __builtin_amdgcn_readfirstlane(__shfl(c, 0)) + seg_lo;
-                    if (c >= seg_hi) {
-                        shard = (shard + 1) % kQueues;
-                        if (++tried == kQueues) exhausted = true;
-                        continue;
-                    }
-                    q_next = c;
-                    q_end = min(c + chunk, seg_hi);
-                }
-                const uint32_t avail = q_end - q_next;
-                const uint32_t r = rank_below(idle);
-                const bool take = slot < 0 && r < avail;
-                const unsigned long long took = __ballot(take);
-                if (take) { slot = (int)(q_next + r); fresh = true; }
-                q_next += (uint32_t)__popcll(took);
-                idle &= ~took;
-            }
-            if (fresh) {
-                nlive++;
-#ifdef RT_PROFILE
-                iters = 0;
-#endif
-                if (FIRST) {
-                    o = S.cam;
-                    d = primary_dir(S, (int)first_ray<FIRST>(pa.map, (uint32_t)slot), pa);
-                } else {
-                    const float4 *rp = geo + (size_t)slot * 2;
-                    const float4 r0 = rp[0];
-                    const float2 r1 = *reinterpret_cast<const float2 *>(rp + 1);
-                    o = v3(r0.x, r0.y, r0.z);
-                    d = v3(r0.w, r1.x, r1.y);
-                }
-                ix = 1 / d.x; iy = 1 / d.y; iz = 1 / d.z;
-                begin_ray();
-                bad = 0;
-                // the reference order at once for a non-finite 1/d component (the literal slab fold) or
-                // origin: a NaN origin passes every slab test bounded by c0 (the order-free search would
-                // visit the whole tree) while the reference stops at its first, NaN, hit
-                ex = force_exact || !(__builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz) &&
-                                      __builtin_isfinite(o.x) && __builtin_isfinite(o.y) && __builtin_isfinite(o.z));
-            }
-            redo[0] += (uint32_t)__popcll(__ballot(fresh && ex));
-        }
-        if (!__ballot(slot >= 0)) {
-            if (exhausted) break;
-            continue;
-        }
-        // ---- one iteration advances both chains of a lane: its pending leaf's next triangle and its
-        // next internal node.  Both records are loaded first (one memory round trip for both); lanes
-        // without one load record 0 (in cache, unused).
-        const bool do_t = slot >= 0 && ti < te;
-        const bool do_n = slot >= 0 && has_node;
-#ifdef RT_PROFILE
-        fprof[0]++;
-        fprof[1] += __popcll(__ballot(do_t));
-        fprof[2] += __popcll(__ballot(do_n));
-        fprof[3] += __popcll(__ballot(do_t && do_n));
-        fprof[4] += __popcll(__ballot(slot >= 0));
-        fprof[5] += __popcll(__ballot(slot >= 0 && ex));
-        if (slot >= 0 && ++iters == 20000) {
-            const unsigned k = atomicAdd(&g_fdbg_n, 1u);
-            if (k < 16) {
-                float *g = g_fdbg[k];
-                g[0] = o.x; g[1] = o.y; g[2] = o.z; g[3] = d.x; g[4] = d.y; g[5] = d.z;
-                g[6] = c0m; g[7] = best; g[8] = second; g[9] = (float)ex; g[10] = (float)sp; g[11] = (float)bad;
-            }
-        }
-#endif
-#if RT_FREE_MASKED
-        float4 ta, tb, na, nb, nc;
-        float tc;
-        uint2 kids;
-        if (do_t) {
-            const float4 *trec = S.tris + (size_t)ti * 3;
-            ta = trec[0]; tb = trec[1]; tc = trec[2].x;
-        }
-        if (do_n) {
-            const float4 *nrec = S.nodes + (size_t)ref * 4;
-            na = nrec[0]; nb = nrec[1]; nc = nrec[2];
-            kids = *reinterpret_cast<const uint2 *>(nrec + 3);
-        }
-#else
-        const float4 *trec = S.tris + (size_t)(do_t ? ti : 0) * 3;
-        const float4 *nrec = S.nodes + (size_t)(do_n ? ref : 0u) * 4;
-        const float4 ta = trec[0], tb = trec[1];
-        const float tc = trec[2].x;
-        const float4 na = nrec[0], nb = nrec[1], nc = nrec[2];
-        const uint2 kids = *reinterpret_cast<const uint2 *>(nrec + 3);
-#endif
-        if (do_t) {
-            // free: tested against `second` (a triangle at or beyond it changes neither best nor
-            // second; below c0 it is a candidate, scene.cu:162-195 with closest = c0); reference
-            // order: against the running closest, accepted as the reference does
-            float t;
-            const bool ok = ray_triangle_flat(o, d, v3(ta.x, ta.y, ta.z), v3(ta.w, tb.x, tb.y), v3(tb.z, tb.w, tc),
-                                              ex ? best : second, t);
-            const bool lt = ok && (ex || t < best);
-            bad |= (!ex && ok && !(t > best) && !lt) ? 2u : 0u;   // a tie at best, or a NaN t: abandoned below
-            second = ex ? second : (lt ? best : (ok && t > best ? t : second));
-            wn = lt ? ln : wn;
-            index = lt ? S.sphere_count + ti : index;
-            best = lt ? t : best;
-            ti++;
-        }
-        if (do_n) {
-            float n0, n1;
-            bool h0, h1;
-            slab_pair(na, nb, nc, o, ix, iy, iz, ex ? best : c0m, h0, h1, n0, n1);
-            const bool leaf0 = kids.x & kLeaf, leaf1 = kids.y & kLeaf;
-            // free: a hit leaf becomes the pending one if the lane has none, a hit internal child is
-            // next, the rest is pushed
-            const bool free_leaf = ti >= te;
-            const bool tl0 = h0 && leaf0 && free_leaf, tl1 = h1 && leaf1 && free_leaf && !tl0;
-            const bool tn0 = h0 && !leaf0, tn1 = h1 && !leaf1 && !tn0;
-            const bool p0 = h0 && !tl0 && !tn0, p1 = h1 && !tl1 && !tn1;
-            bool nh = tn0 || tn1, nl = tl0 || tl1;
-            uint32_t nref = tn0 ? kids.x : kids.y, lr = tl0 ? kids.x : kids.y;
-            float lnv = tl0 ? n0 : n1;
-            uint2 e0 = p0 ? make_uint2(kids.x, __float_as_uint(n0)) : make_uint2(kids.y, __float_as_uint(n1));
-            int np = (int)p0 + (int)p1;
-            if (__builtin_expect(__ballot(do_n && ex) != 0, 0)) {   // wave-uniform, rare
-                if (ex) {
-                    if (!(__builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz))) {
-                        // 0 * inf may give NaN: the literal per-axis fold (scene.cu:109-132)
-                        h0 = slab(na.x, na.z, nb.x, nb.z, nc.x, nc.z, o, ix, iy, iz, best, n0);
-                        h1 = slab(na.y, na.w, nb.y, nb.w, nc.y, nc.w, o, ix, iy, iz, best, n1);
-                    }
-                    // scene.cu:204-238: push near then far, pop the far child; next entered unless its
-                    // entry distance >= closest
-                    const bool both = h0 && h1, any = h0 || h1;
-                    const bool sel1 = h1 && (!h0 || n0 < n1);
-                    const uint32_t next_ref = sel1 ? kids.y : kids.x;
-                    const float next_t = sel1 ? n1 : n0;
-                    e0 = sel1 ? make_uint2(kids.x, __float_as_uint(n0)) : make_uint2(kids.y, __float_as_uint(n1));
-                    np = both ? 1 : 0;
-                    const bool descend = any && !(next_t >= best);
-                    nl = descend && (next_ref & kLeaf);
-                    nh = descend && !(next_ref & kLeaf);
-                    nref = next_ref;
-                    lr = next_ref;
-                    lnv = next_t;
-                }
-            }
-            has_node = nh;
-            ref = nh ? nref : ref;
-            if (nl) {
-                ln = lnv;
-                ti = (int)(lr & 0xFFFFFFu);
-                te = ti + (int)((lr >> 24) & 0x3Fu);
-            }
-            if (__builtin_expect(__ballot(nl && (lr & kBigLeaf)) != 0, 0)) {
-                if (nl && (lr & kBigLeaf)) leaf_range(S, lr, ti, te);
-            }
-            // pushes without a branch: the first pushed entry at sp, the second (child 1 when both are
-            // pushed) at sp + 1; entries >= kStackLds land on the scratch entry and, rarely, in the
-            // global overflow tail
-            const uint2 e1 = make_uint2(kids.y, __float_as_uint(n1));
-            const bool two = np == 2;
-            if (__builtin_expect(sp + np > kStackMax, 0)) {
-                bad |= 4u;                      // deeper than the reference's stack: start over in its order
-                has_node = false;
-                ti = te = 0;
-                sp = 0;
-            } else {
-                col[min(sp, kStackLds) * kBlock] = e0;
-                col[min(sp + (np > 1 ? 1 : 0), kStackLds) * kBlock] = two ? e1 : e0;
-                if (__builtin_expect(__ballot(np > 0 && sp + np > kStackLds) != 0, 0)) {   // wave-uniform, rare
-                    if (np > 0 && sp >= kStackLds) {
-                        overflow[(sp - kStackLds) * lanes + gl] = e0.x;
-                        overflow[dist_half + (sp - kStackLds) * lanes + gl] = e0.y;
-                    }
-                    if (two && sp + 1 >= kStackLds) {
-                        overflow[(sp + 1 - kStackLds) * lanes + gl] = e1.x;
-                        overflow[dist_half + (sp + 1 - kStackLds) * lanes + gl] = e1.y;
-                    }
-                }
-                sp += np;
-            }
-        }
-        // a tie or a NaN candidate settles nothing: abandon the order-free search now (the ray starts
-        // over in the reference order when it is found done below)
-        if (__builtin_expect(__ballot(!ex && (bad & 2u)) != 0, 0)) {
-            if (!ex && (bad & 2u)) {
-                has_node = false;
-                ti = te = 0;
-                sp = 0;
-            }
-        }
-        // ---- pops.  Free: a lane without a node pops at most twice (a leaf into the free pending
-        // slot, then an internal node; a leaf on top while one is pending waits).  Reference order:
-        // a lane without a node and outside a leaf pops to the next entry nearer than closest
-        // (scene.cu:145-155), entering a leaf or taking the node.
-        for (int k = 0;; k++) {
-#if RT_FREE_FILL
-            // free lanes with a node also pop a leaf on top into a free pending slot (both chains busy)
-            const bool want = slot >= 0 && sp > 0 && (ex ? !has_node && ti >= te : k < 2 && (!has_node || ti >= te));
-#else
-            const bool want = slot >= 0 && !has_node && sp > 0 && (ex ? ti >= te : k < 2);
-#endif
-            if (!__ballot(want)) break;
-            const int top = max(sp - 1, 0);
-            uint2 e = col[min(top, kStackLds) * kBlock];
-            asm volatile("" : "+v"(e.x), "+v"(e.y));   // keep the LDS read an LDS read (see trace_kernel)
-            if (__builtin_expect(__ballot(want && top >= kStackLds) != 0, 0)) {
-                if (want && top >= kStackLds) {
-                    e.x = overflow[(top - kStackLds) * lanes + gl];
-                    e.y = overflow[dist_half + (top - kStackLds) * lanes + gl];
-                }
-            }
-            const bool eleaf = e.x & kLeaf;
-            const bool culled = ex && !(__uint_as_float(e.y) < best);   // scene.cu:150 (distance >= closest)
-            const bool take_leaf = want && !culled && eleaf && ti >= te, take_node = want && !culled && !eleaf && !has_node;
-            sp -= (take_leaf || take_node || (want && culled)) ? 1 : 0;
-            has_node = has_node || take_node;
-            ref = take_node ? e.x : ref;
-            if (take_leaf) {
-                ln = __uint_as_float(e.y);
-                ti = (int)(e.x & 0xFFFFFFu);
-                te = ti + (int)((e.x >> 24) & 0x3Fu);
-            }
-            if (__builtin_expect(__ballot(take_leaf && (e.x & kBigLeaf)) != 0, 0)) {
-                if (take_leaf && (e.x & kBigLeaf)) leaf_range(S, e.x, ti, te);
-            }
-        }
-        // ---- finished rays: the order-free answer when it provably is the reference's, else the
-        // ray starts over in the reference order on this lane
-        const bool done = slot >= 0 && !has_node && ti >= te && sp == 0;
-        const bool keep = ex || (!bad && (index < S.sphere_count || wn < second));
-        const bool again = done && !keep;
-        if (__builtin_expect(__ballot(again) != 0, 0)) {
-            redo[1] += (uint32_t)__popcll(__ballot(again && (bad & 2u)));
-            redo[2] += (uint32_t)__popcll(__ballot(again && (bad & 4u) && !(bad & 2u)));
-            redo[3] += (uint32_t)__popcll(__ballot(again && !bad));
-            if (again) {
-                begin_ray();
-                ex = true;
-                bad = 0;
-            }
-        }
-        slot = done && keep ? -2 - slot : slot;
-    }
-    if (slot <= -2) hits[-2 - slot] = make_float2(best, __int_as_float(index));
-    Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
-    const unsigned long long nl = wave_sum(nlive);
-    if (lane_id() == 0) {
-        if (nl) atomicAdd(&cs->live, nl);
-        for (int k = 0; k < 4; k++)
-            if (redo[k]) atomicAdd(&cs->redo[k], (unsigned long long)redo[k]);
-    }
-#ifdef RT_PROFILE
-    if (lane_id() == 0)
-        for (int i = 0; i < 8; i++) atomicAdd(&g_fprof[FIRST ? 0 : 1][i], fprof[i]);
-#endif
-    if (tspan) {
-        __syncthreads();
-        if (threadIdx.x == 0) atomicMax(&tspan[kSpanSlots + blockIdx.x % kSpanSlots], (unsigned long long)wall_clock64());
-    }
 }
 
 // One ray's shading (scene.cu:376-485) at `slot`: environment lookup on a miss, otherwise
@@ -1682,16 +1279,9 @@ struct rt_renderer {
     // shade/reorder (INLINE), saving the hit round trip and the trace launch per bounce.
     bool inline_hits = false;
     int fused_upto = -1;              // fused reorder at bounces <= this (when not `fused`)
-    // RTAMD_FREE_TRACE=1 (experiment, measured slower): closest hits by the order-free trace, which
-    // runs the rays it cannot settle in the reference order (launch_trace).
-    // RTAMD_FORCE_RETRACE=1 (tests): the order-free kernel runs every ray in the reference order.
-    bool free_trace = std::getenv("RTAMD_FREE_TRACE") && std::atoi(std::getenv("RTAMD_FREE_TRACE")) != 0;
-    // bounces from which the order-free trace runs (earlier ones: the reference-order trace_kernel)
-    int free_from = std::getenv("RTAMD_FREE_FROM") ? std::atoi(std::getenv("RTAMD_FREE_FROM")) : 0;
-    bool force_retrace = std::getenv("RTAMD_FORCE_RETRACE") && std::atoi(std::getenv("RTAMD_FORCE_RETRACE")) != 0;
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
-    DevBuf<float4> spheres, scene_geo, mats;   // scene_geo: child-pair node records, then triangles
+    DevBuf<float4> spheres, tris, mats, nodes;
     DevBuf<uint16_t> mat_idx;
     DevBuf<int2> big;
     DevBuf<float> env, fb;
@@ -1843,21 +1433,11 @@ struct rt_renderer {
         ds.root_ref = nn > 0 ? ref_of(0) : (kLeaf | 0u);
         if (big_h.empty()) big_h.push_back(make_int2(0, 0));
         if ((rc = spheres.upload(sc->spheres, sc->sphere_count, s0))) return rc;
-        // Nodes then triangles in one allocation (the trace addresses both by a 32-bit byte offset
-        // from the node base), + one float4 of slack: traversal reads 64 B at a triangle record
-        // (48 B) like at a node.
-        // (at least one triangle record: the order-free trace loads record 0 on lanes without a leaf)
-        const size_t geo_n = rec_h.size() + std::max<size_t>((size_t)sc->triangle_count * 3, 3) + 1;
-        if (geo_n * sizeof(float4) > 0xFFFFFFFFull)
-            return rtamd::fail(RT_E_INVALID, "scene too large: BVH records + triangles exceed 4 GB");
-        if ((rc = scene_geo.alloc(geo_n))) return rc;
-        if (!rec_h.empty())
-            HIPCHK(hipMemcpyAsync(scene_geo.p, rec_h.data(), rec_h.size() * sizeof(float4), hipMemcpyHostToDevice, s0));
-        if (sc->triangle_count)
-            HIPCHK(hipMemcpyAsync(scene_geo.p + rec_h.size(), sc->triangles, (size_t)sc->triangle_count * 3 * sizeof(float4),
-                                  hipMemcpyHostToDevice, s0));
+        // one float4 of slack: traversal reads 64 B at a triangle record (48 B) like at a node
+        if ((rc = tris.upload(sc->triangles, (size_t)sc->triangle_count * 3, s0, 1))) return rc;
         if ((rc = mats.upload(sc->materials, (size_t)sc->material_count * 3, s0))) return rc;
         if ((rc = mat_idx.upload(sc->material_indices, (size_t)sc->sphere_count + sc->triangle_count, s0))) return rc;
+        if ((rc = nodes.upload(rec_h.data(), rec_h.size(), s0))) return rc;
         if ((rc = big.upload(big_h.data(), big_h.size(), s0))) return rc;
         if ((rc = env.upload(sc->environment_map, (size_t)sc->environment_map_width * sc->environment_map_height * 3, s0)))
             return rc;
@@ -1925,11 +1505,10 @@ struct rt_renderer {
         tm.mark("pass contexts");
         HIPCHK(hipMemsetAsync(fb.p, 0, fb.n * sizeof(float), s0));
         ds.spheres = spheres.p;
-        ds.tris = scene_geo.p + rec_h.size();
-        ds.tri_off = (uint32_t)(rec_h.size() * sizeof(float4));
+        ds.tris = tris.p;
         ds.mat_idx = mat_idx.p;
         ds.mats = mats.p;
-        ds.nodes = scene_geo.p;
+        ds.nodes = nodes.p;
         ds.big_leaves = big.p;
         ds.env = env.p;
         ds.sphere_count = sc->sphere_count;
@@ -1949,21 +1528,6 @@ struct rt_renderer {
         tm.mark("sync");
         tm.report();
         return RT_OK;
-    }
-
-    // The closest hits of bounce b: the order-free trace (trace_free_kernel; rays it cannot settle
-    // start over in the reference order on their lane).  COUNT runs (work counters, compared with the
-    // oracle's Pn/Iv/Tt) and RTAMD_EXACT_TRACE=1 use the reference-order trace_kernel for every ray.
-    template <bool SORTED, bool COUNT, int FIRST>
-    void launch_trace(hipStream_t st, int tgrid, const PassArgs &pa, const float4 *geo, const uint32_t *lv,
-                      uint32_t *qbase, int b, float2 *hits, uint32_t *ovf, unsigned long long *tspan) {
-        uint32_t *q = qbase + (size_t)b * kQueues * kQueueStride;
-        if (COUNT || !free_trace || b < free_from)
-            hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa, geo, lv, q,
-                               hits, ovf, ctr.p, tspan);
-        else
-            hipLaunchKernelGGL((trace_free_kernel<FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa, geo, lv, q, hits, ovf,
-                               ctr.p, tspan, (int)force_retrace);
     }
 
     // Pass p of `while (remaining_rays)` (raytracing.cu:222-254) on context c; the pass's
@@ -2011,12 +1575,13 @@ struct rt_renderer {
                 HIPCHK(hipEventRecord(e0, st));
             }
             const uint32_t *lv = c.live.p + b;
+            uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
             const bool last = b + 1 == bounces;
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
-            launch_trace<SORTED, COUNT, FIRST>(st, tgrid, pa, c.geo[cur].p, lv, c.queue.p, b, c.hits.p, c.overflow.p, \
-                                               tspan ? tspan + kSpanWords * b : nullptr);                            \
+            hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr); \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
@@ -2163,6 +1728,7 @@ struct rt_renderer {
         const int sgrid = std::max(1, std::min(grid, cus * RT_SHADE_BPC));
         const uint32_t seed_term = 279220567u * (uint32_t)(c.t_rem * 20 + b);
         const uint32_t *lv = c.live.p + b;
+        uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
         const int last = b + 1 == bounces;
         const int cur = c.t_cur;
         if (!last) {
@@ -2175,14 +1741,14 @@ struct rt_renderer {
 #define RT_TS(COUNT)                                                                                           \
     do {                                                                                                           \
         if (b == 0) {                                                                                              \
-            launch_trace<true, COUNT, 2>(st, tgrid, pa, c.geo[cur].p, lv, c.queue.p, b, c.hits.p, c.overflow.p,     \
-                                         nullptr);                                                                 \
+            hipLaunchKernelGGL((trace_kernel<true, COUNT, 2>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
             hipLaunchKernelGGL((shade_kernel<true, COUNT, 2, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
                                pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
                                seed_term, last, ctr.p, nullptr);                                                   \
         } else {                                                                                                   \
-            launch_trace<true, COUNT, 0>(st, tgrid, pa, c.geo[cur].p, lv, c.queue.p, b, c.hits.p, c.overflow.p,     \
-                                         nullptr);                                                                 \
+            hipLaunchKernelGGL((trace_kernel<true, COUNT, 0>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
             hipLaunchKernelGGL((shade_kernel<true, COUNT, 0, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
                                pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
                                seed_term, last, ctr.p, c.gslot[cur].p);                                            \
@@ -2304,9 +1870,11 @@ struct rt_renderer {
         const PassArgs pa{1, 0u, FastDiv::of(1), FastDiv::of((uint32_t)width), SlotMap::identity()};
         const int tgrid = std::min(blocks_for(n), trace_blocks);
         if (counters)
-            launch_trace<false, true, 0>(s0, tgrid, pa, geo.p, live.p, queue.p, 0, hits.p, overflow.p, nullptr);
+            hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
+                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr);
         else
-            launch_trace<false, false, 0>(s0, tgrid, pa, geo.p, live.p, queue.p, 0, hits.p, overflow.p, nullptr);
+            hipLaunchKernelGGL((trace_kernel<false, false, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
+                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr);
         HIPCHK(hipGetLastError());
         std::vector<float2> h((size_t)n);
         HIPCHK(hipMemcpyAsync(h.data(), hits.p, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, s0));
@@ -2460,26 +2028,6 @@ struct rt_renderer {
             }
             std::memset(pr, 0, sizeof(pr));
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));
-            unsigned long long fp[2][8];
-            HIPCHK(hipMemcpyFromSymbol(fp, HIP_SYMBOL(g_fprof), sizeof(fp)));
-            for (int f = 0; f < 2; f++) {
-                const unsigned long long *q = fp[f];
-                const double it = (double)std::max(1ull, q[0]);
-                std::fprintf(stderr, "RT_FPROFILE %s iters %llu tri_lanes/iter %.2f node_lanes/iter %.2f both/iter %.2f "
-                             "active/iter %.2f reference_order/iter %.3f\n", f ? "later" : "bounce0", q[0], q[1] / it, q[2] / it,
-                             q[3] / it, q[4] / it, q[5] / it);
-            }
-            std::memset(fp, 0, sizeof(fp));
-            HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_fprof), fp, sizeof(fp)));
-            unsigned int dn = 0;
-            float dg[16][12];
-            HIPCHK(hipMemcpyFromSymbol(&dn, HIP_SYMBOL(g_fdbg_n), sizeof(dn)));
-            HIPCHK(hipMemcpyFromSymbol(dg, HIP_SYMBOL(g_fdbg), sizeof(dg)));
-            std::fprintf(stderr, "RT_FDEBUG rays past 20000 iterations: %u\n", dn);
-            for (unsigned k = 0; k < std::min(dn, 16u); k++)
-                std::fprintf(stderr, "RT_FDEBUG o %.9g %.9g %.9g d %.9g %.9g %.9g c0m %.9g best %.9g second %.9g ex %g sp %g bad %g\n",
-                             dg[k][0], dg[k][1], dg[k][2], dg[k][3], dg[k][4], dg[k][5], dg[k][6], dg[k][7], dg[k][8], dg[k][9],
-                             dg[k][10], dg[k][11]);
         }
 #endif
         if (st) {
@@ -2490,11 +2038,7 @@ struct rt_renderer {
             for (const Counters &x : slots) {
                 c.live += x.live; c.pn += x.pn; c.iv += x.iv; c.tt += x.tt; c.st += x.st;
                 c.hits += x.hits; c.misses += x.misses; c.hits_sphere += x.hits_sphere;
-                for (int k = 0; k < 4; k++) c.redo[k] += x.redo[k];
             }
-            if (std::getenv("RTAMD_TIMING"))
-                std::fprintf(stderr, "rt_renderer run: %llu live segments, re-traced: %llu (1/d), %llu (tie/NaN), %llu (stack), "
-                             "%llu (entry check)\n", c.live, c.redo[0], c.redo[1], c.redo[2], c.redo[3]);
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, t_begin, t_end));
             st->kernel_ms = ms;
