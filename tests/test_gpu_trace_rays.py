@@ -4,7 +4,10 @@ oracle's restatement of the sphere loop + bvh_closest_hit_distance (scene.cu:338
 Besides random rays this drives the corner cases a render reaches only by chance: direction
 components that are exactly zero (1/d = inf, so the slab planes give 0 * inf = NaN when the
 origin lies on one), axis-aligned rays, origins exactly on triangle vertices (on box faces),
-and rays that start inside the geometry.  Bit-exact t and index, exact traversal counters.
+rays that start inside the geometry, and non-finite origins and directions (a NaN hit distance
+becomes the next bounce's NaN origin: lamp's glass makes them in a render; the reference then
+accepts the first triangle it tests with a NaN t).  Bit-exact t and index (NaN = NaN), exact
+traversal counters, through both builds of the kernel (with and without the counters).
 """
 import numpy as np
 import pytest
@@ -52,7 +55,19 @@ def _ray_sets(orc, rng, n):
     d[np.arange(n), rng.integers(0, 3, n)] = 0.0
     sets["vertex_origin_zero_component"] = np.hstack([vo, _unit(d)])
     sets["vertex_origin_axis"] = np.hstack([vo, axes[rng.integers(0, 6, n)]])
+    nf = np.hstack([o, _unit(rng.normal(size=(n, 3)))]).astype(np.float32)
+    k = np.arange(n)
+    nf[k % 4 == 0, rng.integers(0, 3)] = np.nan                       # NaN origin component
+    nf[k % 4 == 1, 3 + rng.integers(0, 3)] = np.nan                   # NaN direction component
+    nf[k % 4 == 2, rng.integers(0, 3)] = np.inf                       # infinite origin component
+    nf[k % 4 == 3, 3:6] = 0.0                                         # zero direction
+    sets["non_finite"] = nf
     return sets
+
+
+def _same(t_o, i_o, t_g, i_g):
+    both_nan = np.isnan(t_o) & np.isnan(t_g)
+    return np.nonzero(((t_o.view(np.uint32) != t_g.view(np.uint32)) & ~both_nan) | (i_o != i_g))[0]
 
 
 @pytest.mark.parametrize("scene,use_bvh", [("cornell", True), ("cornell_plus", True), ("spheres", True),
@@ -65,12 +80,16 @@ def test_trace_rays_bitexact(scene, use_bvh):
     for name, rays in _ray_sets(orc, rng, 20000).items():
         t_o, i_o, s_o = orc.closest_hit(rays)
         t_g, i_g, s_g = R.trace_rays(dev, rays, counters=True)
-        bad = np.nonzero((t_o.view(np.uint32) != t_g.view(np.uint32)) | (i_o != i_g))[0]
+        bad = _same(t_o, i_o, t_g, i_g)
         assert bad.size == 0, "%s/%s: %d rays differ, first %s: oracle (%r, %d) gpu (%r, %d)" % (
             scene, name, bad.size, bad[:1], t_o[bad[0]], i_o[bad[0]], t_g[bad[0]], i_g[bad[0]])
         for k in ("nodes_popped", "internal_visits", "triangle_tests", "sphere_tests"):
             assert s_o[k] == s_g[k], (scene, name, k, s_o[k], s_g[k])
-        assert (i_o >= 0).any()
+        # the render's build of the kernel (no counters)
+        t_r, i_r, _ = R.trace_rays(dev, rays)
+        bad = _same(t_o, i_o, t_r, i_r)
+        assert bad.size == 0, "%s/%s (render build): %d rays differ" % (scene, name, bad.size)
+        assert name == "non_finite" or (i_o >= 0).any()
 
 
 def test_trace_rays_empty_and_single():
