@@ -110,6 +110,8 @@ constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are i
 constexpr int kRefillFirst = RT_REFILL_FIRST;   // same at bounce 0: a whole wave of consecutive primary rays
                                                 // (~3 pixels) starts together and stays in lockstep
 constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffer set each)
+constexpr int kStaggerUs = 2000;       // staggered start of the first passes in flight (rt_renderer::run)
+constexpr int kStaggerMinPasses = 8;   // ...for renders of at least this many passes
 // Persistent trace grid as a % of the resident trace workgroups: the passes in flight share the
 // chip, so each pass's trace takes 200 % / (passes in flight), at least RT_TRACE_OCC_MIN and at most
 // 100 % (20 in flight: 15 %; A/B at 20 in flight: 40 % 7.51, 30 % 7.41, 20 % 7.37, 15 % 7.33,
@@ -999,6 +1001,13 @@ __global__ __launch_bounds__(kBlock) void sort_rank_kernel(const uint8_t *__rest
         }
     }
 }
+// One wave that waits `ticks` of the device's constant-rate wall clock (a pass's staggered start,
+// rt_renderer::run); bounded by its argument.
+__global__ void delay_kernel(unsigned long long ticks) {
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 __global__ void set_count_kernel(uint32_t *__restrict__ dst, uint32_t v, const uint32_t *__restrict__ src) {
     if (threadIdx.x == 0) *dst = src ? *src : v;
 }
@@ -1288,6 +1297,9 @@ struct rt_renderer {
     DevBuf<Counters> ctr;
     DevBuf<unsigned long long> tspans;   // per run: [pass][bounce] trace-launch wall-clock spans (event timing on)
     int wall_khz = 0;                    // device wall clock rate (wall_clock64 ticks per ms)
+    // staggered start of the first passes in flight (run); RTAMD_STAGGER_US overrides, 0 = off
+    int stagger_us = std::getenv("RTAMD_STAGGER_US") ? std::max(0, std::min(20000, std::atoi(std::getenv("RTAMD_STAGGER_US"))))
+                                                    : kStaggerUs;
     PassCtx ctx[kInflight];
     int pass_hint = 0;                // rt_render: the passes this renderer will ever run (0: any)
     int trace_blocks = 0;             // persistent trace_kernel grid of the current run
@@ -1916,8 +1928,8 @@ struct rt_renderer {
         hipStream_t s0 = stream();
         if (pass_events && tspans.n < (size_t)std::max(count, 1) * kSpanWords * (bounces + 1)) {
             if (int rc = tspans.alloc((size_t)std::max(count, 1) * kSpanWords * (bounces + 1))) return rc;
-            if (!wall_khz) HIPCHK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, device));
         }
+        if (!wall_khz) HIPCHK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, device));
         HIPCHK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) * kCtrSlots, s0));
         HIPCHK(hipEventRecord(t_begin, s0));
         for (int k = 1; k < inflight; k++) HIPCHK(hipStreamWaitEvent(ctx[k].stream, t_begin, 0));
@@ -1993,10 +2005,20 @@ struct rt_renderer {
                 return rtamd::fail(RT_E_INVALID, "tile exchange: " + std::to_string(bad) +
                                                  " global slots had no owner's byte (the exchange must sum every owner's array)");
         } else {
+            // Staggered start of the first passes in flight: pass k (k < passes in flight) begins
+            // k * RTAMD_STAGGER_US later (a one-wave wait on its stream).  Started together, the first
+            // passes run their heavy bounces 0-1 side by side and then their latency-bound tails side
+            // by side; staggered, one pass's tail overlaps another's heavy bounces (A/B, 20-pass batch,
+            // 6 rounds: 7.23 -> 7.14 ms/pass at 2 ms, 7.15 at 3 ms, 7.22 at 4 ms; the same as delaying
+            // the host's enqueue by 2 ms per pass; a full frame and a 13-pass share unchanged).  Later
+            // passes start when a context frees, staggered already.  Off for short renders.
+            const long stagger_ticks = count >= kStaggerMinPasses ? (long)stagger_us * wall_khz / 1000 : 0;
             for (int k = 0; k < count; k++) {
                 PassCtx &c = ctx[k % inflight];
                 const int p = pass_begin + k * stride;
                 float *sums = sums_of(c, k);
+                if (k > 0 && k < inflight && stagger_ticks > 0)
+                    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, c.stream, (unsigned long long)(k * stagger_ticks));
                 const int rc = enqueue_pass(c, p, sums, sorted,
                                             pass_events ? tspans.p + (size_t)k * kSpanWords * (bounces + 1) : nullptr);
                 if (rc) return rc;
