@@ -110,8 +110,6 @@ constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are i
 constexpr int kRefillFirst = RT_REFILL_FIRST;   // same at bounce 0: a whole wave of consecutive primary rays
                                                 // (~3 pixels) starts together and stays in lockstep
 constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffer set each)
-constexpr int kGroupBelow = 32768;     // tail bounces: trace_group_kernel below this many live rays
-constexpr int kGroupQueue = 32;        // its queue word: in the bounce's queue line set, apart from the shards'
 constexpr int kStaggerUs = 2000;       // staggered start of the first passes in flight (rt_renderer::run)
 constexpr int kStaggerMinPasses = 8;   // ...for renders of at least this many passes
 // Persistent trace grid as a % of the resident trace workgroups: the passes in flight share the
@@ -155,7 +153,6 @@ __device__ unsigned long long g_prof[2][12];   // [bounce 0, later bounces]
 
 struct Counters {                     // device-side work counters (u64, one atomic per wave)
     unsigned long long live, pn, iv, tt, st, hits, misses, hits_sphere;
-    unsigned long long exact_retraces;   // trace_group_kernel: rays traced again in the reference order
 };
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
@@ -319,9 +316,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
-                                                       unsigned long long *__restrict__ tspan, uint32_t skip_below = 0) {
-    // skip_below: fewer live rays than this are trace_group_kernel's (launched beside this one)
-    if (*live_count < skip_below) return;
+                                                       unsigned long long *__restrict__ tspan) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
@@ -572,263 +567,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         for (int i = 0; i < 12; i++)
             if (i != 10) atomicAdd(&g_prof[FIRST ? 0 : 1][i], prof[i]);
 #endif
-}
-
-// ---------------------------------------------------------------- tail bounces: 16 lanes per ray
-// A tail bounce (a few per cent of the rays live) waits for its longest ray: ~450 dependent steps of
-// ~0.75 us on a nearly idle chip (profiles/r03/oracle_bounce_profile_teapot.json, pmc_traffic.json:
-// 0.36-0.44 ms per tail trace launch serialised).  Here a group of 16 lanes traces one ray, up to 16
-// nodes / triangles per step, in no particular order: the reference's far-first traversal culls
-// almost nothing, so the search below tests every slab-hit subtree bounded only by the sphere
-// loop's closest c0 (0.7-2.5 % more work, tools/experiments/exhaustive_probe.cpp), and its answer is
-// the reference's whenever the least candidate t* is unique, no candidate t is NaN, 1/d and the
-// origin are finite, and the winner's leaf entry distance is below the least t of the other
-// candidates (DESIGN.md §8 "Order-free traversal": the reference's closest stays above that until it
-// tests the winner, and entry distances only grow down the tree).  A ray that fails the check, or
-// whose frontier outgrows the group's LDS stack, is traced again in the reference order by the
-// group's first lane (exact_closest_hit).
-constexpr int kGroup = 16;                    // lanes per ray
-constexpr int kGroupStack = 128;              // LDS items per group (>= kStackMax for the exact path)
-constexpr uint32_t kTriItem = 0x80000000u;    // item = triangle index | kTriItem, else a record index
-
-// bvh_closest_hit_distance (scene.cu:134-241) for one lane, on a stack of {ref, entry distance} in
-// `st`: the reference's visit order, pushes and culls, on the child-pair records.
-__device__ __forceinline__ void exact_closest_hit(const DevScene &S, V3 o, V3 d, float ix, float iy, float iz, uint2 *st,
-                                               float &closest, int &index) {
-    const bool fin = __builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz);
-    int sp = 0;
-    st[sp++] = make_uint2(S.root_ref, 0u);     // the root, popped at distance 0
-    while (sp > 0) {
-        const uint2 e = st[--sp];
-        if (__uint_as_float(e.y) >= closest) continue;
-        const uint32_t ref = e.x;
-        if (ref & kLeaf) {
-            int ti, te;
-            leaf_range(S, ref, ti, te);
-            for (int i = ti; i < te; i++) {
-                const float4 *r = S.tris + (size_t)i * 3;
-                const float4 q0 = r[0], q1 = r[1];
-                const float q2 = r[2].x;
-                float t;
-                if (ray_triangle_flat(o, d, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), closest, t)) {
-                    closest = t;
-                    index = S.sphere_count + i;
-                }
-            }
-        } else {
-            const float4 *r = S.nodes + (size_t)ref * 4;
-            const float4 a = r[0], b = r[1], c = r[2];
-            const uint2 kids = *reinterpret_cast<const uint2 *>(r + 3);
-            float n0, n1;
-            bool h0, h1;
-            if (fin) {
-                slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, n0, n1);
-            } else {
-                h0 = slab(a.x, a.z, b.x, b.z, c.x, c.z, o, ix, iy, iz, closest, n0);
-                h1 = slab(a.y, a.w, b.y, b.w, c.y, c.w, o, ix, iy, iz, closest, n1);
-            }
-            // scene.cu:204-238: both hit -> the nearer pushed first, the farther popped next
-            if (h0 && h1) {
-                if (n0 < n1) {
-                    st[sp++] = make_uint2(kids.x, __float_as_uint(n0));
-                    st[sp++] = make_uint2(kids.y, __float_as_uint(n1));
-                } else {
-                    st[sp++] = make_uint2(kids.y, __float_as_uint(n1));
-                    st[sp++] = make_uint2(kids.x, __float_as_uint(n0));
-                }
-            } else if (h0) {
-                st[sp++] = make_uint2(kids.x, __float_as_uint(n0));
-            } else if (h1) {
-                st[sp++] = make_uint2(kids.y, __float_as_uint(n1));
-            }
-        }
-    }
-}
-
-// Items of a hit child: its record (internal) or its triangles (leaf), counted per lane.
-__device__ __forceinline__ uint32_t child_items(const DevScene &S, bool hit, uint32_t ref, int &ti) {
-    if (!hit) return 0;
-    if (!(ref & kLeaf)) return 1;
-    int te;
-    leaf_range(S, ref, ti, te);
-    return (uint32_t)(te - ti);
-}
-
-__global__ __launch_bounds__(kBlock) void trace_group_kernel(DevScene S, const float4 *__restrict__ geo,
-                                                             const uint32_t *__restrict__ live_count,
-                                                             uint32_t *__restrict__ queue, float2 *__restrict__ hits,
-                                                             Counters *__restrict__ ctr, int force_exact, uint32_t below) {
-    if (*live_count >= below) return;   // the wave-per-64-rays trace_kernel's (launched beside this one)
-    __shared__ uint2 gstack[kBlock / kGroup][kGroupStack];
-    uint2 *st = gstack[threadIdx.x / kGroup];
-    const int gi = threadIdx.x % kGroup;                       // lane within the group
-    const int lead = (int)(lane_id() & ~(uint32_t)(kGroup - 1)); // the group's first lane in the wave
-    const unsigned long long gmask = 0xFFFFull << lead;
-    const uint32_t L = __builtin_amdgcn_readfirstlane(*live_count);
-    int slot = -1;                      // group-uniform from here on
-    bool exhausted = false;
-    V3 o{0, 0, 0}, d{0, 0, 0};
-    float ix = 0, iy = 0, iz = 0, c0 = 0, c0m = 0;
-    int index0 = -1;                    // the sphere loop's answer
-    int sp = 0;                         // group stack depth (group-uniform)
-    float best = 0, second = 0, wn = 0; // this lane's candidates (see the reduction below)
-    int index = -1;
-    bool bad = false;                   // a tie at this lane's best, or a NaN t
-    unsigned nlive = 0, nexact = 0;
-    while (true) {
-        if (slot < 0 && !exhausted) {   // a group without a ray takes the next slot
-            uint32_t s = 0;
-            if (gi == 0) s = atomicAdd(queue, 1u);
-            s = (uint32_t)__shfl((int)s, lead);
-            if (s >= L) {
-                exhausted = true;
-            } else {
-                slot = (int)s;
-                nlive += gi == 0 ? 1u : 0u;
-                const float4 *rp = geo + (size_t)slot * 2;
-                const float4 r0 = rp[0];
-                const float2 r1 = *reinterpret_cast<const float2 *>(rp + 1);
-                o = v3(r0.x, r0.y, r0.z);
-                d = v3(r0.w, r1.x, r1.y);
-                ix = 1 / d.x; iy = 1 / d.y; iz = 1 / d.z;
-                c0 = 1e30f;
-                index0 = -1;
-                for (int i = 0; i < S.sphere_count; i++) {
-                    const float4 sph = S.spheres[i];
-                    float t;
-                    if (ray_sphere(o, d, v3(sph.x, sph.y, sph.z), sph.w, c0, t)) { c0 = t; index0 = i; }
-                }
-                c0m = __int_as_float(__float_as_int(c0) - 1);   // c0 >= 0.005 > 0
-                best = second = c0;
-                wn = 0;
-                index = index0;
-                bad = false;
-                sp = 0;
-                const bool exact = force_exact || !(__builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz) &&
-                                                    __builtin_isfinite(o.x) && __builtin_isfinite(o.y) && __builtin_isfinite(o.z));
-                if (exact) {
-                    sp = -1;                    // straight to the reference order
-                } else if (S.root_ref & kLeaf) {
-                    int ti, te;
-                    leaf_range(S, S.root_ref, ti, te);
-                    if (te - ti > kGroupStack) {
-                        sp = -1;
-                    } else {
-                        for (int k = gi; k < te - ti; k += kGroup) st[k] = make_uint2(kTriItem | (uint32_t)(ti + k), 0u);
-                        sp = te - ti;
-                    }
-                } else {
-                    if (gi == 0) st[0] = make_uint2(S.root_ref, 0u);
-                    sp = 1;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-        }
-        if (!__ballot(slot >= 0)) {
-            if (!__ballot(!exhausted)) break;
-            continue;
-        }
-        if (slot >= 0 && sp > 0) {
-            // ---- one step: the group's top items, one per lane
-            const int take = min(sp, kGroup);
-            const bool has = gi < take;
-            const uint2 it = has ? st[sp - 1 - gi] : make_uint2(0u, 0u);
-            sp -= take;
-            const bool tri = has && (it.x & kTriItem);
-            const uint32_t id = it.x & ~kTriItem;
-            const float4 *rec = tri ? S.tris + (size_t)id * 3 : S.nodes + (size_t)(has ? id : 0u) * 4;
-            const float4 a = rec[0], b = rec[1], c = rec[2];
-            const uint2 kids = *reinterpret_cast<const uint2 *>(rec + 3);
-            uint32_t cnt0 = 0, cnt1 = 0;
-            int t0i = 0, t1i = 0;
-            float n0 = 0, n1 = 0;
-            if (tri) {
-                // against this lane's second: a triangle at or beyond it is neither the winner nor the
-                // least other candidate of the group (this lane holds two candidates below it)
-                float t;
-                const bool ok = ray_triangle_flat(o, d, v3(a.x, a.y, a.z), v3(a.w, b.x, b.y), v3(b.z, b.w, c.x), second, t);
-                const bool lt = ok && t < best;
-                bad = bad || (ok && !(t > best) && !lt);   // a tie at this lane's best, or a NaN t
-                second = lt ? best : (ok && t > best ? t : second);
-                wn = lt ? __uint_as_float(it.y) : wn;
-                index = lt ? S.sphere_count + (int)id : index;
-                best = lt ? t : best;
-            } else if (has) {
-                bool h0, h1;
-                slab_pair(a, b, c, o, ix, iy, iz, c0m, h0, h1, n0, n1);   // entry < c0 and within the far plane
-                cnt0 = child_items(S, h0, kids.x, t0i);
-                cnt1 = child_items(S, h1, kids.y, t1i);
-            }
-            // the group's pushes: an exclusive scan of the item counts over its 16 lanes
-            const uint32_t cnt = cnt0 + cnt1;
-            uint32_t incl = cnt;
-#pragma unroll
-            for (int off = 1; off < kGroup; off <<= 1) {
-                const uint32_t v = (uint32_t)__shfl_up((int)incl, off, kGroup);
-                incl += gi >= off ? v : 0u;
-            }
-            const int total = __shfl((int)incl, lead + kGroup - 1);
-            if (sp + total > kGroupStack) {
-                sp = -1;                        // frontier too wide: the reference order below
-            } else {
-                int w = sp + (int)(incl - cnt);
-                if (cnt0) {
-                    if (kids.x & kLeaf) {
-                        for (uint32_t k = 0; k < cnt0; k++) st[w + k] = make_uint2(kTriItem | (uint32_t)(t0i + k), __float_as_uint(n0));
-                    } else {
-                        st[w] = make_uint2(kids.x, __float_as_uint(n0));
-                    }
-                    w += (int)cnt0;
-                }
-                if (cnt1) {
-                    if (kids.y & kLeaf) {
-                        for (uint32_t k = 0; k < cnt1; k++) st[w + k] = make_uint2(kTriItem | (uint32_t)(t1i + k), __float_as_uint(n1));
-                    } else {
-                        st[w] = make_uint2(kids.y, __float_as_uint(n1));
-                    }
-                }
-                sp += total;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        // ---- finished rays: the group's least candidate, checked, else the reference order
-        const bool fin = slot >= 0 && sp <= 0;
-        if (__ballot(fin)) {
-            float B = best;
-#pragma unroll
-            for (int off = kGroup / 2; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, kGroup));
-            const unsigned long long own = __ballot(fin && best == B && B < c0) & gmask;
-            const int owner = own ? (int)__builtin_ctzll(own) : lead;
-            float S2 = lane_id() == (uint32_t)owner ? second : best;
-#pragma unroll
-            for (int off = kGroup / 2; off > 0; off >>= 1) S2 = fminf(S2, __shfl_xor(S2, off, kGroup));
-            const float wno = __shfl(wn, owner);
-            const int ido = __shfl(index, owner);
-            const bool any_bad = (__ballot(fin && bad) & gmask) != 0;
-            const bool keep = sp == 0 && (!(B < c0) || (__popcll(own) == 1 && !any_bad && wno < S2));
-            float tr = keep ? (B < c0 ? B : c0) : c0;
-            int ir = keep ? (B < c0 ? ido : index0) : index0;
-            if (fin && !keep && gi == 0) {      // the reference order, on the group's first lane
-                exact_closest_hit(S, o, d, ix, iy, iz, st, tr, ir);
-                nexact++;
-            }
-            if (fin && gi == 0) hits[slot] = make_float2(tr, __int_as_float(ir));
-            if (fin) slot = -1;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-    }
-    Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
-    const unsigned long long nl = wave_sum(nlive), ne = wave_sum(nexact);
-    if (lane_id() == 0) {
-        if (nl) atomicAdd(&cs->live, nl);
-        if (ne) atomicAdd(&cs->exact_retraces, ne);
-    }
 }
 
 // One ray's shading (scene.cu:376-485) at `slot`: environment lookup on a miss, otherwise
@@ -1559,11 +1297,6 @@ struct rt_renderer {
     DevBuf<Counters> ctr;
     DevBuf<unsigned long long> tspans;   // per run: [pass][bounce] trace-launch wall-clock spans (event timing on)
     int wall_khz = 0;                    // device wall clock rate (wall_clock64 ticks per ms)
-    // bounces >= 1 with fewer live rays than this: trace_group_kernel (16 lanes per ray) instead of
-    // trace_kernel; RTAMD_GROUP_BELOW overrides (0 = never).  RTAMD_FORCE_EXACT=1 (tests): the group
-    // kernel traces every ray in the reference order.
-    int group_below = std::getenv("RTAMD_GROUP_BELOW") ? std::max(0, std::atoi(std::getenv("RTAMD_GROUP_BELOW"))) : kGroupBelow;
-    bool force_exact = std::getenv("RTAMD_FORCE_EXACT") && std::atoi(std::getenv("RTAMD_FORCE_EXACT")) != 0;
     // staggered start of the first passes in flight (run); RTAMD_STAGGER_US overrides, 0 = off
     int stagger_us = std::getenv("RTAMD_STAGGER_US") ? std::max(0, std::min(20000, std::atoi(std::getenv("RTAMD_STAGGER_US"))))
                                                     : kStaggerUs;
@@ -1858,14 +1591,9 @@ struct rt_renderer {
             const bool last = b + 1 == bounces;
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
-        if (!inline_hits) {                                                                                      \
-            const uint32_t gb = !COUNT && !FIRST ? (uint32_t)group_below : 0u;                                  \
+        if (!inline_hits)                                                                                        \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr, gb); \
-            if (gb)                                                                                              \
-                hipLaunchKernelGGL(trace_group_kernel, dim3(std::max(1, trace_blocks_max / 2)), dim3(kBlock), 0, st, ds, c.geo[cur].p, lv, \
-                                   q + kGroupQueue, c.hits.p, ctr.p, (int)force_exact, gb);                      \
-        }                                                                                                        \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr); \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
