@@ -51,7 +51,7 @@ def main():
         occ = "8 waves/SIMD (64 VGPRs)" if r else "— (no trace kernel)" if "spheres" in name else "8 waves/SIMD"
         cpu = "%.1f (%d, %s)" % (cb["frame_s"], cb["cores"], "extrapolated" if cb.get("extrapolated") else "full frame") \
             if cb.get("frame_s") is not None else "—"
-        print("| %s | 1 | %s | %s | %.0f | %.0f | %s | %s | %s | %s | %s | profiles/r03/%s |" % (
+        print("| %s | 1 | %s | %s | %.0f | %.0f | %s | %s | %s | %s | %s | profiles/r03/final/%s |" % (
             name, d.get("render_wall_ms"), "%.1f" % km if km else "—", d["value"], d["config"]["nominal_mrays_per_s"],
             "%.0f (%.3f)" % (fr["achieved"], fr["frac"]) if fr else "—", "%.3f" % va["frac"] if va else "—", occ,
             d.get("bit_exact_vs_oracle"), cpu, f))
