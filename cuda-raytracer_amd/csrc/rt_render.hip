@@ -110,7 +110,8 @@ constexpr int kRefill = RT_REFILL;   // refill a wave once this many lanes are i
 constexpr int kRefillFirst = RT_REFILL_FIRST;   // same at bounce 0: a whole wave of consecutive primary rays
                                                 // (~3 pixels) starts together and stays in lockstep
 constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffer set each)
-constexpr int kStaggerUs = 2000;       // staggered start of the first passes in flight (rt_renderer::run)
+constexpr int kStaggerUs = 4000;       // staggered start of the first passes in flight (rt_renderer::run):
+constexpr int kStaggerGroup = 4;       // the first kStaggerGroup together, then one every kStaggerUs
 constexpr int kStaggerMinPasses = 8;   // ...for renders of at least this many passes
 // Persistent trace grid as a % of the resident trace workgroups: the passes in flight share the
 // chip, so each pass's trace takes 200 % / (passes in flight), at least RT_TRACE_OCC_MIN and at most
@@ -2005,20 +2006,25 @@ struct rt_renderer {
                 return rtamd::fail(RT_E_INVALID, "tile exchange: " + std::to_string(bad) +
                                                  " global slots had no owner's byte (the exchange must sum every owner's array)");
         } else {
-            // Staggered start of the first passes in flight: pass k (k < passes in flight) begins
-            // k * RTAMD_STAGGER_US later (a one-wave wait on its stream).  Started together, the first
-            // passes run their heavy bounces 0-1 side by side and then their latency-bound tails side
-            // by side; staggered, one pass's tail overlaps another's heavy bounces (A/B, 20-pass batch,
-            // 6 rounds: 7.23 -> 7.14 ms/pass at 2 ms, 7.15 at 3 ms, 7.22 at 4 ms; the same as delaying
-            // the host's enqueue by 2 ms per pass; a full frame and a 13-pass share unchanged).  Later
-            // passes start when a context frees, staggered already.  Off for short renders.
+            // Staggered start of the first passes in flight: the first kStaggerGroup start together
+            // (they fill the chip), then pass k (k < passes in flight) begins (k - group + 1) *
+            // kStaggerUs later (a one-wave wait on its stream).  Started together, the first passes run
+            // their heavy bounces 0-1 side by side and then their latency-bound tails side by side;
+            // staggered, one pass's tail overlaps another's heavy bounces (A/B: 20-pass batch 7.13 ->
+            // 7.02 ms/pass, through the dist path 7.40 -> 7.19, full frame 6.84 -> 6.74, lamp 20 steps
+            // 13.53 -> 13.32; one pass every 2 ms from pass 1: 7.23 -> 7.14).  Later passes start when a
+            // context frees, staggered already.  Off for short renders.  RTAMD_STAGGER_US /
+            // RTAMD_STAGGER_GROUP override.
             const long stagger_ticks = count >= kStaggerMinPasses ? (long)stagger_us * wall_khz / 1000 : 0;
+            const int stagger_group = std::getenv("RTAMD_STAGGER_GROUP") ? std::max(1, std::atoi(std::getenv("RTAMD_STAGGER_GROUP")))
+                                                                        : kStaggerGroup;
             for (int k = 0; k < count; k++) {
                 PassCtx &c = ctx[k % inflight];
                 const int p = pass_begin + k * stride;
                 float *sums = sums_of(c, k);
-                if (k > 0 && k < inflight && stagger_ticks > 0)
-                    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, c.stream, (unsigned long long)(k * stagger_ticks));
+                if (k >= stagger_group && k < inflight && stagger_ticks > 0)
+                    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, c.stream,
+                                       (unsigned long long)((k - stagger_group + 1) * stagger_ticks));
                 const int rc = enqueue_pass(c, p, sums, sorted,
                                             pass_events ? tspans.p + (size_t)k * kSpanWords * (bounces + 1) : nullptr);
                 if (rc) return rc;
