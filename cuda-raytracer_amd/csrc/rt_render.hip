@@ -1306,6 +1306,7 @@ struct rt_renderer {
     int trace_blocks = 0;             // persistent trace_kernel grid of the current run
     int trace_blocks_max = 0;         // all resident trace workgroups (the overflow stacks are sized for it)
     int nctx = 1;                     // pass contexts allocated (passes in flight)
+    int inflight_cap = kInflight;     // passes in flight allowed (kInflight, or RTAMD_INFLIGHT)
     int cus = 0;
     hipEvent_t t_begin = nullptr, t_end = nullptr;
 
@@ -1477,6 +1478,7 @@ struct rt_renderer {
         // 20 contexts ran a 13-pass share at 12.7 instead of 8.1 ms/pass)
         size_t cap = kInflight;
         if (const char *e = std::getenv("RTAMD_INFLIGHT")) cap = std::min<size_t>(cap, (size_t)std::max(1, std::atoi(e)));
+        inflight_cap = (int)cap;
         if (pass_hint > 0) cap = std::min<size_t>(cap, (size_t)pass_hint);   // a one-shot render of fewer passes
         nctx = !passes ? 0 : (int)std::min<size_t>({cap, (size_t)std::max(1, pass_count()),
                                                     std::max<size_t>(1, mem_free / 2 / ctx_bytes)});
@@ -2013,9 +2015,11 @@ struct rt_renderer {
             // staggered, one pass's tail overlaps another's heavy bounces (A/B: 20-pass batch 7.13 ->
             // 7.02 ms/pass, through the dist path 7.40 -> 7.19, full frame 6.84 -> 6.74, lamp 20 steps
             // 13.53 -> 13.32; one pass every 2 ms from pass 1: 7.23 -> 7.14).  Later passes start when a
-            // context frees, staggered already.  Off for short renders.  RTAMD_STAGGER_US /
-            // RTAMD_STAGGER_GROUP override.
-            const long stagger_ticks = count >= kStaggerMinPasses ? (long)stagger_us * wall_khz / 1000 : 0;
+            // context frees, staggered already.  Only for renders of at least as many passes as may be
+            // in flight (kInflight, or RTAMD_INFLIGHT): a shorter one (cornell_plus' 13 passes of 3 ms)
+            // only waits (3.04 -> 3.49 ms/pass), as does a 13-pass rank share at 16 in flight (7.52 -> 7.61).  RTAMD_STAGGER_US / RTAMD_STAGGER_GROUP
+            // override.
+            const long stagger_ticks = count >= inflight_cap && count >= kStaggerMinPasses ? (long)stagger_us * wall_khz / 1000 : 0;
             const int stagger_group = std::getenv("RTAMD_STAGGER_GROUP") ? std::max(1, std::atoi(std::getenv("RTAMD_STAGGER_GROUP")))
                                                                         : kStaggerGroup;
             for (int k = 0; k < count; k++) {
