@@ -653,6 +653,11 @@ __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &p
 // Ray state lives in slot order (the reorder moves it), so every access here is coalesced.  A
 // ray's radiance goes to acc[ray id] (pixel-major, what accumulation reads) when it terminates
 // or after the last bounce.
+__device__ __forceinline__ unsigned long long match_bucket(uint32_t b, bool valid);
+
+// counts (or null): the reorder's per-tile bucket histogram (sort_hist_kernel's output) counted here
+// as the buckets are made, so the bounce needs no histogram launch and no second read of the
+// buckets; the blocks then walk whole reorder tiles instead of 256-slot strides.
 template <bool SORTED, bool COUNT, int FIRST, bool FUSED, bool INLINE>
 __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
                                                        float4 *__restrict__ tc, const uint32_t *__restrict__ rid,
@@ -660,12 +665,12 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
                                                        const uint32_t *__restrict__ live_count,
                                                        const float2 *__restrict__ hits, uint32_t seed_term, int last,
                                                        Counters *__restrict__ ctr,
-                                                       const uint32_t *__restrict__ seed_of = nullptr) {
+                                                       const uint32_t *__restrict__ seed_of = nullptr,
+                                                       uint32_t *__restrict__ counts = nullptr, int tiles = 0) {
     const int L = (int)__builtin_amdgcn_readfirstlane(*live_count);
     unsigned hit = 0, miss = 0, hit_sphere = 0;
-    for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
-        const int slot = base + threadIdx.x;
-        if (slot >= L) continue;
+    // one slot's shading and new state; returns its bucket
+    auto shade_slot = [&](int slot) -> uint32_t {
         const Shaded sh = shade_one<SORTED, FIRST, INLINE>(S, pa, slot, geo, tc, rid, hits, seed_term, seed_of);
         const V3 no = sh.no, nd = sh.nd, T = sh.T, C = sh.C;
         miss += sh.kind == 0;
@@ -679,7 +684,34 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
         }
         if (dead || last) acc[sh.ray] = tcv;
         else if (!FUSED) tc[slot] = tcv;   // FUSED: the reorder replays the shading instead
-        if (!last) bkt[slot] = (uint8_t)(dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u));
+        const uint32_t bk = dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u);
+        if (!last) bkt[slot] = (uint8_t)bk;
+        return bk;
+    };
+    if (counts && !last) {
+        __shared__ uint32_t h[kBuckets];
+        const int R = tile_rounds(L), span = kBlock * R;
+        for (int tile = blockIdx.x; tile * span < L; tile += gridDim.x) {
+            for (int b = threadIdx.x; b < kBuckets; b += kBlock) h[b] = 0;
+            __syncthreads();
+            const int base = tile * span;
+            const int rounds = min(R, (L - base + kBlock - 1) / kBlock);   // block-uniform: the last tile is short
+            for (int r = 0; r < rounds; r++) {
+                const int slot = base + r * kBlock + threadIdx.x;
+                const bool valid = slot < L;
+                const uint32_t bk = valid ? shade_slot(slot) : 0u;
+                const unsigned long long peers = match_bucket(bk, valid);
+                if (valid && rank_below(peers) == 0) atomicAdd(&h[bk], (uint32_t)__popcll(peers));
+            }
+            __syncthreads();
+            for (int b = threadIdx.x; b < kBuckets; b += kBlock) counts[(size_t)b * tiles + tile] = h[b];
+            __syncthreads();
+        }
+    } else {
+        for (int base = blockIdx.x * kBlock; base < L; base += gridDim.x * kBlock) {
+            const int slot = base + threadIdx.x;
+            if (slot < L) (void)shade_slot(slot);
+        }
     }
     if (INLINE) {   // no trace kernel ran: the live segments (and the root pop, the sphere tests) count here
         Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
@@ -1299,6 +1331,8 @@ struct rt_renderer {
     DevBuf<unsigned long long> tspans;   // per run: [pass][bounce] trace-launch wall-clock spans (event timing on)
     int wall_khz = 0;                    // device wall clock rate (wall_clock64 ticks per ms)
     // staggered start of the first passes in flight (run); RTAMD_STAGGER_US overrides, 0 = off
+    // the reorder's bucket histogram counted inside the shade kernel (RTAMD_SHADE_HIST=0: its own launch)
+    bool shade_hist = !std::getenv("RTAMD_SHADE_HIST") || std::atoi(std::getenv("RTAMD_SHADE_HIST")) != 0;
     int stagger_us = std::getenv("RTAMD_STAGGER_US") ? std::max(0, std::min(20000, std::atoi(std::getenv("RTAMD_STAGGER_US"))))
                                                     : kStaggerUs;
     PassCtx ctx[kInflight];
@@ -1592,6 +1626,7 @@ struct rt_renderer {
             const uint32_t *lv = c.live.p + b;
             uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
             const bool last = b + 1 == bounces;
+            uint32_t *hist = shade_hist && !last ? c.sort_counts.p : nullptr;   // the shade kernel counts the buckets
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
@@ -1601,15 +1636,15 @@ struct rt_renderer {
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
                                ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,  \
-                               seed_term, (int)last, ctr.p);                                                     \
+                               seed_term, (int)last, ctr.p, nullptr, hist, tiles);                               \
         else if (fused || b <= fused_upto)                                                                       \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, false>), dim3(sgrid), dim3(kBlock), 0, \
                                st, ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
-                               seed_term, (int)last, ctr.p);                                                     \
+                               seed_term, (int)last, ctr.p, nullptr, hist, tiles);                               \
         else                                                                                                     \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, false, false>), dim3(sgrid), dim3(kBlock), 0, \
                                st, ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
-                               seed_term, (int)last, ctr.p);                                                     \
+                               seed_term, (int)last, ctr.p, nullptr, hist, tiles);                               \
     } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
     do {                                                                                                         \
@@ -1635,8 +1670,9 @@ struct rt_renderer {
                     if (!s0 || !s1) return rtamd::fail(RT_E_HIP, "hipEventCreate failed");
                     HIPCHK(hipEventRecord(s0, st));
                 }
-                hipLaunchKernelGGL(sort_hist_kernel, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, lv, tiles,
-                                   c.sort_counts.p);
+                if (!hist)
+                    hipLaunchKernelGGL(sort_hist_kernel, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, lv, tiles,
+                                       c.sort_counts.p);
                 hipLaunchKernelGGL(sort_scan_kernel, dim3(kBuckets), dim3(kBlock), 0, st, c.sort_counts.p, lv, tiles,
                                    c.sort_offsets.p, c.sort_totals.p, c.live.p + b + 1);
                 if (fused || b <= fused_upto) {
