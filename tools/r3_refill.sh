@@ -1,0 +1,7 @@
+# Round 3: trace refill threshold with the shaped stagger and the fused histogram
+export TMPDIR=/tmp
+OUT=gpurun_out/r3_refill
+mkdir -p $OUT
+AB_ARGS="--no-extras --steps 20 --warmup 5" timeout -k 10 800 python tools/ab.py 4 default rf20 rf28 > $OUT/ab_20.txt 2>&1; tail -4 $OUT/ab_20.txt
+AB_ARGS="--no-extras" timeout -k 10 600 python tools/ab.py 3 default rf20 rf28 > $OUT/ab_frame.txt 2>&1; tail -4 $OUT/ab_frame.txt
+echo done
