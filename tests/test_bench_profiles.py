@@ -67,3 +67,49 @@ def test_roofline_restated_on_exclusive_launches():
     if pmc:
         assert abs(roof["traffic_frac"] - pmc["trace_bytes_per_launch"] / 0.7e-3 / 1e9 / 8000.0) < 1e-3
     assert roof["logical_per_step"]["achieved"] > 0
+
+
+def _final_lines():
+    d = os.path.join(REPO, "profiles", "r03", "final")
+    out = {}
+    for f in sorted(os.listdir(d)):
+        if f.startswith("bench_") and f.endswith(".json"):
+            with open(os.path.join(d, f)) as fh:
+                out[f] = json.loads(fh.read().strip().splitlines()[-1])
+    return out
+
+
+def test_closing_lines_every_config_bit_exact():
+    """Round 3's closing measurement (profiles/r03/final): a line per BASELINE config, each with its pass-0
+    framebuffer hash equal to the oracle's and its fractions at most one."""
+    lines = _final_lines()
+    for name in ("bench_cornell.json", "bench_cornell_plus.json", "bench_spheres.json", "bench_teapot.json",
+                 "bench_teapotnosort.json", "bench_lamp.json", "bench_lampnosort.json", "bench_teapot_steps20.json"):
+        assert name in lines, name
+        d = lines[name]
+        assert d["bit_exact_vs_oracle"] is True, name
+        assert d["value"] > 0 and d["ms_per_step"] > 0
+        roof = d.get("roofline")
+        if roof and roof.get("frac") is not None:   # traced configs (spheres has no trace kernel)
+            assert 0 < roof["frac"] <= 1, name
+            if roof.get("traffic_frac") is not None:   # configs with a committed PMC record (not cornell)
+                assert 0 < roof["traffic_frac"] <= 1, name
+                assert 0 < roof["frame"]["frac"] <= 1 and 0 < roof["valu"]["frac"] <= 1, name
+    assert lines["bench_teapot_steps20.json"]["steps"] == 20 and lines["bench_teapot_steps20.json"]["warmup"] == 5
+
+
+def test_closing_exclusive_launch_agrees_with_the_profiler():
+    """The bench's exclusive trace launch duration (device wall clock, one atomic per workgroup) and the
+    profiler's average dispatch duration of the same launches agree within 10 %."""
+    roof = _final_lines()["bench_teapot.json"]["roofline"]
+    a, b = roof["ms_per_launch"], roof["pmc_run"]["ms_per_launch"]
+    assert abs(a - b) / b < 0.10, (a, b)
+
+
+def test_results_table_from_committed_files():
+    import subprocess
+    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "results_table.py"),
+                          os.path.join(REPO, "profiles", "r03", "final")], capture_output=True, text=True, check=True).stdout
+    rows = [r for r in out.splitlines() if r.startswith("| ") and " | 1 | " in r]
+    assert len(rows) == 7, out                      # 5 configs, teapot and lamp in both sort modes
+    assert all("| True |" in r for r in rows)
