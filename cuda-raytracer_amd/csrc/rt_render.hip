@@ -64,6 +64,12 @@ namespace {
 #ifndef RT_QUEUES
 #define RT_QUEUES 8
 #endif
+#ifndef RT_ROOT_STEP
+#define RT_ROOT_STEP 0
+#endif
+#ifndef RT_TOP_LEVELS
+#define RT_TOP_LEVELS 4
+#endif
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 constexpr int kStackLds = RT_STACK_LDS; // stack entries per lane kept in LDS (deeper: global)
 constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138)
@@ -128,6 +134,10 @@ constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFF
 constexpr int kSpanSlots = 8;
 constexpr int kSpanWords = 2 * kSpanSlots;
 constexpr uint32_t kLeaf = 0x80000000u, kBigLeaf = 0x40000000u;
+// The top kTopLevels levels of internal nodes get the first records (breadth-first; at most
+// 2^kTopLevels records with the root's padding record), which the trace kernel keeps in LDS.
+constexpr int kTopLevels = RT_ROOT_STEP >= 3 ? RT_TOP_LEVELS : 0;
+constexpr int kTopRecs = 1 << kTopLevels;
 
 struct DevScene {
     const float4 *spheres;            // center.xyz, radius
@@ -139,6 +149,7 @@ struct DevScene {
     const float *env;                 // env_h * env_w * 3
     int sphere_count, env_w, env_h, width, height;
     uint32_t root_ref;
+    uint32_t top_recs;                // records [0, top_recs): the top BVH levels (kTopLevels), breadth-first
     V3 cam, tl, sr, su, min_coord, inv_dim;
     float inv_w, inv_h;
 };
@@ -319,6 +330,11 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
                                                        unsigned long long *__restrict__ tspan) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
+#if RT_ROOT_STEP >= 3
+    __shared__ float4 top[kTopRecs * 4];
+    for (uint32_t k = threadIdx.x; k < S.top_recs * 4; k += kBlock) top[k] = S.nodes[k];
+    __syncthreads();
+#endif
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
     // before its first wave and the stream's marker packets (what rocprofv3 reports)
@@ -350,6 +366,125 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     unsigned pn = 0, iv = 0, tt = 0, nlive = 0;
 #ifdef RT_PROFILE
     unsigned long long prof[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    // One internal node's step (both children's slabs, scene.cu:196-225) on the record {a, b, c, kids}:
+    // pushes the near child when both are hit, enters the next one; returns whether the lane needs
+    // its next node from the stack.
+    auto node_step = [&](float4 a, float4 b, float4 c, uint2 kids) -> bool {
+        if (COUNT) iv++;
+        float t0, t1;
+        bool h0, h1;
+        slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
+        if (__builtin_expect(wave_nonfinite, 0)) {
+            // some lane's 1/d has an infinite component (0 * inf may give NaN): the literal
+            // per-axis fold for those lanes
+            float u0, u1;
+            const bool g0 = slab(a.x, a.z, b.x, b.z, c.x, c.z, o, ix, iy, iz, closest, u0);
+            const bool g1 = slab(a.y, a.w, b.y, b.w, c.y, c.w, o, ix, iy, iz, closest, u1);
+            if (!finite_inv) { h0 = g0; h1 = g1; t0 = u0; t1 = u1; }
+        }
+        // The reference pushes the hit children near then far (scene.cu:204-225) and pops the
+        // top: with both hit the far child is next and the near one stays on the stack; with
+        // one hit that one is next.  Next is entered unless its entry distance >= closest.
+        // (one predicate picks both children, logical not bitwise predicates: A/B 7.50-7.65 ->
+        // 7.28-7.37 ms/pass with the refill-time non-finite ballot above)
+        const bool both = h0 && h1, any = h0 || h1;
+        // next = child 1 iff it is the far child of two hits (t0 < t1; a tie makes child 1 the
+        // near one) or the only hit; the other child is the near one, pushed when both hit
+        const bool sel1 = h1 && (!h0 || t0 < t1);
+        const uint32_t next_ref = sel1 ? kids.y : kids.x, near_ref = sel1 ? kids.x : kids.y;
+        const float next_t = sel1 ? t1 : t0, near_t = sel1 ? t0 : t1;
+        // the near child is written either way (above the top when not pushed; entry
+        // kStackLds is a scratch slot), so the push needs no branch
+        col[min(sp, kStackLds) * kBlock] = make_uint2(near_ref, __float_as_uint(near_t));
+        if (__builtin_expect(both && sp >= kStackLds, 0)) {
+            overflow[(sp - kStackLds) * lanes + gl] = near_ref;
+            overflow[dist_half + (sp - kStackLds) * lanes + gl] = __float_as_uint(near_t);
+        }
+        if (both) sp++;
+        ref = any ? next_ref : ref;
+        const bool descend = any && !(next_t >= closest);
+        bool need = !descend;
+        if (descend) {
+            if (COUNT) pn++;
+            if (ref & kLeaf) {
+                leaf_range(S, ref, ti, te);
+                need = ti == te;
+            }
+        }
+        return need;
+    };
+    // Pop to the next entry nearer than closest (scene.cu:147-152), the per-entry decisions as
+    // selects: the LDS entry is read for every popping lane (an empty stack reads entry 0,
+    // unused), only the rare overflow-stack entries and big-leaf ranges take a branch (round 3:
+    // the nested if/else form cost ~27 SALU + 7 branches more per loop body).
+    auto pop_loop = [&](bool need) {
+        while (need) {
+            PROF(10, 1);
+            const bool empty = sp == 0;
+            sp = empty ? 0 : sp - 1;
+            uint2 e = col[min(sp, kStackLds) * kBlock];
+            // opaque: keeps the LDS read an LDS read (the compiler would otherwise fold it and the
+            // rare overflow read below into one flat load through a selected pointer)
+            asm volatile("" : "+v"(e.x), "+v"(e.y));
+            if (__builtin_expect(__ballot(sp >= kStackLds) != 0, 0)) {   // wave-uniform, rare
+                if (sp >= kStackLds) {
+                    e.x = overflow[(sp - kStackLds) * lanes + gl];
+                    e.y = overflow[dist_half + (sp - kStackLds) * lanes + gl];
+                }
+            }
+            const bool take = !empty && !(__uint_as_float(e.y) >= closest);
+            slot = empty ? -2 - slot : slot;   // done; {closest, index} stored at the next refill or at exit
+            ref = take ? e.x : ref;
+            if (COUNT) pn += take ? 1u : 0u;
+            const bool leaf = take && (ref & kLeaf);
+            if (__builtin_expect(leaf && (ref & kBigLeaf), 0)) {
+                leaf_range(S, ref, ti, te);
+            } else {
+                ti = leaf ? (int)(ref & 0xFFFFFFu) : ti;
+                te = leaf ? ti + (int)((ref >> 24) & 0x3Fu) : te;
+            }
+            need = !empty && (!take || (leaf && ti == te));
+        }
+    };
+#if RT_ROOT_STEP && RT_ROOT_STEP < 3
+    // The root's child-pair record is the same for every ray: read once into scalar registers, so
+    // a refill runs its fresh lanes' root step without a memory round trip and they enter the loop
+    // one level down (later bounces: ~1 of ~19 steps per ray).
+    const bool root_internal = !(S.root_ref & kLeaf);
+    float4 ra{0, 0, 0, 0}, rb{0, 0, 0, 0}, rc{0, 0, 0, 0};
+    uint2 rk{0, 0};
+    if (root_internal) {
+        const float4 *rr = S.nodes + (size_t)S.root_ref * 4;
+        const float4 x0 = rr[0], x1 = rr[1], x2 = rr[2];
+        const uint2 k = *reinterpret_cast<const uint2 *>(rr + 3);
+#define RT_U(v) __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)))
+        ra = make_float4(RT_U(x0.x), RT_U(x0.y), RT_U(x0.z), RT_U(x0.w));
+        rb = make_float4(RT_U(x1.x), RT_U(x1.y), RT_U(x1.z), RT_U(x1.w));
+        rc = make_float4(RT_U(x2.x), RT_U(x2.y), RT_U(x2.z), RT_U(x2.w));
+#undef RT_U
+        rk = make_uint2(__builtin_amdgcn_readfirstlane(k.x), __builtin_amdgcn_readfirstlane(k.y));
+    }
+#if RT_ROOT_STEP >= 2
+    // ...and the root's two children's records (when both are internal): a second step at refill for
+    // the lanes standing on one of them
+    const bool kids_internal = root_internal && !(rk.x & kLeaf) && !(rk.y & kLeaf);
+    float4 xa{0, 0, 0, 0}, xb{0, 0, 0, 0}, xc{0, 0, 0, 0}, ya{0, 0, 0, 0}, yb{0, 0, 0, 0}, yc{0, 0, 0, 0};
+    uint2 xk{0, 0}, yk{0, 0};
+    if (kids_internal) {
+#define RT_U(v) __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)))
+#define RT_U4(v) make_float4(RT_U(v.x), RT_U(v.y), RT_U(v.z), RT_U(v.w))
+        const float4 *px = S.nodes + (size_t)rk.x * 4, *py = S.nodes + (size_t)rk.y * 4;
+        const float4 x0 = px[0], x1 = px[1], x2 = px[2], y0 = py[0], y1 = py[1], y2 = py[2];
+        const uint2 kx = *reinterpret_cast<const uint2 *>(px + 3), ky = *reinterpret_cast<const uint2 *>(py + 3);
+        xa = RT_U4(x0); xb = RT_U4(x1); xc = RT_U4(x2);
+        ya = RT_U4(y0); yb = RT_U4(y1); yc = RT_U4(y2);
+#undef RT_U4
+#undef RT_U
+        xk = make_uint2(__builtin_amdgcn_readfirstlane(kx.x), __builtin_amdgcn_readfirstlane(kx.y));
+        yk = make_uint2(__builtin_amdgcn_readfirstlane(ky.x), __builtin_amdgcn_readfirstlane(ky.y));
+    }
+#endif
 #endif
     while (true) {
         // ---- refill idle lanes (wave-uniform control flow)
@@ -427,6 +562,38 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             // one ballot per refill instead of one per node step; the flag stays set until the next
             // refill even if that ray has finished (the per-lane fold below is exact for every lane)
             wave_nonfinite = __ballot(slot >= 0 && !finite_inv) != 0;
+#if RT_ROOT_STEP >= 3
+            // every lane standing on a top-level node (fresh lanes at the root, and any lane that has
+            // popped back to one) steps it now on the LDS copy of its record, until none is left
+            while (true) {
+                const bool at_top = slot >= 0 && !(ti < te) && ref < S.top_recs;   // leaf refs have bit 31
+                if (!__ballot(at_top)) break;
+                bool need = false;
+                if (at_top) {
+                    const float4 *r = top + ref * 4;
+                    const float4 k3 = r[3];
+                    need = node_step(r[0], r[1], r[2], make_uint2(__float_as_uint(k3.x), __float_as_uint(k3.y)));
+                }
+                pop_loop(need);
+            }
+#elif RT_ROOT_STEP
+            if (root_internal && __ballot(fresh && slot >= 0)) {
+                bool need = false;
+                if (fresh && slot >= 0) need = node_step(ra, rb, rc, rk);
+                pop_loop(need);
+#if RT_ROOT_STEP >= 2
+                const bool on_x = slot >= 0 && !(ti < te) && ref == rk.x, on_y = slot >= 0 && !(ti < te) && ref == rk.y;
+                if (kids_internal && __ballot(on_x || on_y)) {   // any lane about to step a depth-1 node
+                    need = false;
+                    if (on_x || on_y) {
+                        const float4 a = on_x ? xa : ya, b = on_x ? xb : yb, c = on_x ? xc : yc;
+                        need = node_step(a, b, c, on_x ? xk : yk);
+                    }
+                    pop_loop(need);
+                }
+#endif
+            }
+#endif
         }
         if (!__ballot(slot >= 0)) {
             if (exhausted) break;
@@ -468,82 +635,12 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             index = hit ? S.sphere_count + ti : index;
             need = ++ti == te;
         } else {
-            if (COUNT) iv++;
-            float t0, t1;
-            bool h0, h1;
-            slab_pair(a, b, c, o, ix, iy, iz, closest, h0, h1, t0, t1);
-            if (__builtin_expect(wave_nonfinite, 0)) {
-                // some lane's 1/d has an infinite component (0 * inf may give NaN): the literal
-                // per-axis fold for those lanes
-                float u0, u1;
-                const bool g0 = slab(a.x, a.z, b.x, b.z, c.x, c.z, o, ix, iy, iz, closest, u0);
-                const bool g1 = slab(a.y, a.w, b.y, b.w, c.y, c.w, o, ix, iy, iz, closest, u1);
-                if (!finite_inv) { h0 = g0; h1 = g1; t0 = u0; t1 = u1; }
-            }
-            // The reference pushes the hit children near then far (scene.cu:204-225) and pops the
-            // top: with both hit the far child is next and the near one stays on the stack; with
-            // one hit that one is next.  Next is entered unless its entry distance >= closest.
-            // (one predicate picks both children, logical not bitwise predicates: A/B 7.50-7.65 ->
-            // 7.28-7.37 ms/pass with the refill-time non-finite ballot above)
-            const bool both = h0 && h1, any = h0 || h1;
-            // next = child 1 iff it is the far child of two hits (t0 < t1; a tie makes child 1 the
-            // near one) or the only hit; the other child is the near one, pushed when both hit
-            const bool sel1 = h1 && (!h0 || t0 < t1);
-            const uint32_t next_ref = sel1 ? kids.y : kids.x, near_ref = sel1 ? kids.x : kids.y;
-            const float next_t = sel1 ? t1 : t0, near_t = sel1 ? t0 : t1;
-            // the near child is written either way (above the top when not pushed; entry
-            // kStackLds is a scratch slot), so the push needs no branch
-            col[min(sp, kStackLds) * kBlock] = make_uint2(near_ref, __float_as_uint(near_t));
-            if (__builtin_expect(both && sp >= kStackLds, 0)) {
-                overflow[(sp - kStackLds) * lanes + gl] = near_ref;
-                overflow[dist_half + (sp - kStackLds) * lanes + gl] = __float_as_uint(near_t);
-            }
-            if (both) sp++;
-            ref = any ? next_ref : ref;
-            const bool descend = any && !(next_t >= closest);
-            need = !descend;
-            if (descend) {
-                if (COUNT) pn++;
-                if (ref & kLeaf) {
-                    leaf_range(S, ref, ti, te);
-                    need = ti == te;
-                }
-            }
+            need = node_step(a, b, c, kids);
         }
 #ifdef RT_PROFILE
         if (__ballot(need)) PROF(5, 1);
 #endif
-        // Pop to the next entry nearer than closest (scene.cu:147-152), the per-entry decisions as
-        // selects: the LDS entry is read for every popping lane (an empty stack reads entry 0,
-        // unused), only the rare overflow-stack entries and big-leaf ranges take a branch (round 3:
-        // the nested if/else form cost ~27 SALU + 7 branches more per loop body).
-        while (need) {
-            PROF(10, 1);
-            const bool empty = sp == 0;
-            sp = empty ? 0 : sp - 1;
-            uint2 e = col[min(sp, kStackLds) * kBlock];
-            // opaque: keeps the LDS read an LDS read (the compiler would otherwise fold it and the
-            // rare overflow read below into one flat load through a selected pointer)
-            asm volatile("" : "+v"(e.x), "+v"(e.y));
-            if (__builtin_expect(__ballot(sp >= kStackLds) != 0, 0)) {   // wave-uniform, rare
-                if (sp >= kStackLds) {
-                    e.x = overflow[(sp - kStackLds) * lanes + gl];
-                    e.y = overflow[dist_half + (sp - kStackLds) * lanes + gl];
-                }
-            }
-            const bool take = !empty && !(__uint_as_float(e.y) >= closest);
-            slot = empty ? -2 - slot : slot;   // done; {closest, index} stored at the next refill or at exit
-            ref = take ? e.x : ref;
-            if (COUNT) pn += take ? 1u : 0u;
-            const bool leaf = take && (ref & kLeaf);
-            if (__builtin_expect(leaf && (ref & kBigLeaf), 0)) {
-                leaf_range(S, ref, ti, te);
-            } else {
-                ti = leaf ? (int)(ref & 0xFFFFFFu) : ti;
-                te = leaf ? ti + (int)((ref >> 24) & 0x3Fu) : te;
-            }
-            need = !empty && (!take || (leaf && ti == te));
-        }
+        pop_loop(need);
     }
     if (slot <= -2) hits[-2 - slot] = make_float2(closest, __int_as_float(index));
     Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
@@ -1426,7 +1523,7 @@ struct rt_renderer {
         // order is unchanged.
         const int nn = sc->bvh_node_count;
         std::vector<int> rec(nn, -1);
-        int nrec = 0;
+        int nrec = 0, top_recs = 0;
         if (nn > 0 && !is_leaf(sc->bvh[0])) {
             rec[0] = 0;
             nrec = 2;                   // record 1: padding, the root has no sibling
@@ -1436,6 +1533,30 @@ struct rt_renderer {
             // run past the per-lane overflow stack, so it is refused here
             std::vector<std::pair<int, int>> todo{{0, 0}};
             int visited = 0;
+            // the top kTopLevels levels first, breadth-first (the trace kernel's LDS copy); their
+            // deepest level's subtrees then depth-first as below
+            for (size_t h = 0; kTopLevels > 1 && h < todo.size(); h++) {
+                const int i = todo[h].first, depth = todo[h].second;
+                if (depth + 1 >= kTopLevels) continue;
+                if (++visited > nn) return rtamd::fail(RT_E_INVALID, "BVH is not a tree");
+                const rt_bvh_node &nd = sc->bvh[i];
+                if (nd.child1 < 0 || nd.child2 >= nn || nd.child1 >= nn || nd.child2 < 0)
+                    return rtamd::fail(RT_E_INVALID, "BVH child index out of range");
+                const bool in1 = !is_leaf(sc->bvh[nd.child1]), in2 = !is_leaf(sc->bvh[nd.child2]);
+                if (in1) rec[nd.child1] = nrec;
+                if (in2) rec[nd.child2] = nrec + 1;
+                if (in1 || in2) nrec += 2;
+                if (in1) todo.push_back({nd.child1, depth + 1});
+                if (in2) todo.push_back({nd.child2, depth + 1});
+                todo[h].first = -1;         // done
+            }
+            top_recs = nrec;
+            if (kTopLevels > 1) {           // the nodes left (the deepest top level) depth-first, in order
+                std::vector<std::pair<int, int>> rest;
+                for (auto it = todo.rbegin(); it != todo.rend(); ++it)
+                    if (it->first >= 0) rest.push_back(*it);
+                todo.swap(rest);
+            }
             while (!todo.empty()) {
                 const int i = todo.back().first, depth = todo.back().second;
                 todo.pop_back();
@@ -1479,6 +1600,7 @@ struct rt_renderer {
             q[3].z = q[3].w = 0.0f;
         }
         ds.root_ref = nn > 0 ? ref_of(0) : (kLeaf | 0u);
+        ds.top_recs = kTopLevels > 0 ? (uint32_t)std::min(top_recs, nrec) : 0u;
         if (big_h.empty()) big_h.push_back(make_int2(0, 0));
         if ((rc = spheres.upload(sc->spheres, sc->sphere_count, s0))) return rc;
         // one float4 of slack: traversal reads 64 B at a triangle record (48 B) like at a node
