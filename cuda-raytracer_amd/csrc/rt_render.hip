@@ -64,12 +64,6 @@ namespace {
 #ifndef RT_QUEUES
 #define RT_QUEUES 8
 #endif
-#ifndef RT_ROOT_STEP
-#define RT_ROOT_STEP 0
-#endif
-#ifndef RT_TOP_LEVELS
-#define RT_TOP_LEVELS 4
-#endif
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 constexpr int kStackLds = RT_STACK_LDS; // stack entries per lane kept in LDS (deeper: global)
 constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138)
@@ -134,10 +128,6 @@ constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFF
 constexpr int kSpanSlots = 8;
 constexpr int kSpanWords = 2 * kSpanSlots;
 constexpr uint32_t kLeaf = 0x80000000u, kBigLeaf = 0x40000000u;
-// The top kTopLevels levels of internal nodes get the first records (breadth-first; at most
-// 2^kTopLevels records with the root's padding record), which the trace kernel keeps in LDS.
-constexpr int kTopLevels = RT_ROOT_STEP >= 3 ? RT_TOP_LEVELS : 0;
-constexpr int kTopRecs = 1 << kTopLevels;
 
 struct DevScene {
     const float4 *spheres;            // center.xyz, radius
@@ -149,7 +139,6 @@ struct DevScene {
     const float *env;                 // env_h * env_w * 3
     int sphere_count, env_w, env_h, width, height;
     uint32_t root_ref;
-    uint32_t top_recs;                // records [0, top_recs): the top BVH levels (kTopLevels), breadth-first
     V3 cam, tl, sr, su, min_coord, inv_dim;
     float inv_w, inv_h;
 };
@@ -330,11 +319,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
                                                        unsigned long long *__restrict__ tspan) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
-#if RT_ROOT_STEP >= 3
-    __shared__ float4 top[kTopRecs * 4];
-    for (uint32_t k = threadIdx.x; k < S.top_recs * 4; k += kBlock) top[k] = S.nodes[k];
-    __syncthreads();
-#endif
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
     // before its first wave and the stream's marker packets (what rocprofv3 reports)
@@ -447,10 +431,14 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             need = !empty && (!take || (leaf && ti == te));
         }
     };
-#if RT_ROOT_STEP && RT_ROOT_STEP < 3
     // The root's child-pair record is the same for every ray: read once into scalar registers, so
     // a refill runs its fresh lanes' root step without a memory round trip and they enter the loop
-    // one level down (later bounces: ~1 of ~19 steps per ray).
+    // one level down (later bounces: ~1 of ~19 steps per ray).  Round 3, A/B on one box: teapot frame
+    // 6.81 -> 6.67 ms/pass, driver-style 20 steps 7.05 -> 6.92, lamp 13.27 -> 12.90.  Also measured:
+    // the root's two children's records in scalar registers too (a second step at refill; 6.71, 6.86,
+    // 12.95: no better) and an LDS copy of the top 3-5 levels (breadth-first records) stepped at
+    // refill until no lane stands on one (7.00-7.04, 7.15-7.19, 12.86-12.98: the refill's record
+    // registers push the kernel into scratch spills); revision b72e94c has both (RT_ROOT_STEP=2/3).
     const bool root_internal = !(S.root_ref & kLeaf);
     float4 ra{0, 0, 0, 0}, rb{0, 0, 0, 0}, rc{0, 0, 0, 0};
     uint2 rk{0, 0};
@@ -465,27 +453,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 #undef RT_U
         rk = make_uint2(__builtin_amdgcn_readfirstlane(k.x), __builtin_amdgcn_readfirstlane(k.y));
     }
-#if RT_ROOT_STEP >= 2
-    // ...and the root's two children's records (when both are internal): a second step at refill for
-    // the lanes standing on one of them
-    const bool kids_internal = root_internal && !(rk.x & kLeaf) && !(rk.y & kLeaf);
-    float4 xa{0, 0, 0, 0}, xb{0, 0, 0, 0}, xc{0, 0, 0, 0}, ya{0, 0, 0, 0}, yb{0, 0, 0, 0}, yc{0, 0, 0, 0};
-    uint2 xk{0, 0}, yk{0, 0};
-    if (kids_internal) {
-#define RT_U(v) __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)))
-#define RT_U4(v) make_float4(RT_U(v.x), RT_U(v.y), RT_U(v.z), RT_U(v.w))
-        const float4 *px = S.nodes + (size_t)rk.x * 4, *py = S.nodes + (size_t)rk.y * 4;
-        const float4 x0 = px[0], x1 = px[1], x2 = px[2], y0 = py[0], y1 = py[1], y2 = py[2];
-        const uint2 kx = *reinterpret_cast<const uint2 *>(px + 3), ky = *reinterpret_cast<const uint2 *>(py + 3);
-        xa = RT_U4(x0); xb = RT_U4(x1); xc = RT_U4(x2);
-        ya = RT_U4(y0); yb = RT_U4(y1); yc = RT_U4(y2);
-#undef RT_U4
-#undef RT_U
-        xk = make_uint2(__builtin_amdgcn_readfirstlane(kx.x), __builtin_amdgcn_readfirstlane(kx.y));
-        yk = make_uint2(__builtin_amdgcn_readfirstlane(ky.x), __builtin_amdgcn_readfirstlane(ky.y));
-    }
-#endif
-#endif
     while (true) {
         // ---- refill idle lanes (wave-uniform control flow)
         unsigned long long idle = __ballot(slot < 0);
@@ -562,38 +529,11 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             // one ballot per refill instead of one per node step; the flag stays set until the next
             // refill even if that ray has finished (the per-lane fold below is exact for every lane)
             wave_nonfinite = __ballot(slot >= 0 && !finite_inv) != 0;
-#if RT_ROOT_STEP >= 3
-            // every lane standing on a top-level node (fresh lanes at the root, and any lane that has
-            // popped back to one) steps it now on the LDS copy of its record, until none is left
-            while (true) {
-                const bool at_top = slot >= 0 && !(ti < te) && ref < S.top_recs;   // leaf refs have bit 31
-                if (!__ballot(at_top)) break;
-                bool need = false;
-                if (at_top) {
-                    const float4 *r = top + ref * 4;
-                    const float4 k3 = r[3];
-                    need = node_step(r[0], r[1], r[2], make_uint2(__float_as_uint(k3.x), __float_as_uint(k3.y)));
-                }
-                pop_loop(need);
-            }
-#elif RT_ROOT_STEP
-            if (root_internal && __ballot(fresh && slot >= 0)) {
+            if (root_internal && __ballot(fresh && slot >= 0)) {   // the fresh lanes' root step
                 bool need = false;
                 if (fresh && slot >= 0) need = node_step(ra, rb, rc, rk);
                 pop_loop(need);
-#if RT_ROOT_STEP >= 2
-                const bool on_x = slot >= 0 && !(ti < te) && ref == rk.x, on_y = slot >= 0 && !(ti < te) && ref == rk.y;
-                if (kids_internal && __ballot(on_x || on_y)) {   // any lane about to step a depth-1 node
-                    need = false;
-                    if (on_x || on_y) {
-                        const float4 a = on_x ? xa : ya, b = on_x ? xb : yb, c = on_x ? xc : yc;
-                        need = node_step(a, b, c, on_x ? xk : yk);
-                    }
-                    pop_loop(need);
-                }
-#endif
             }
-#endif
         }
         if (!__ballot(slot >= 0)) {
             if (exhausted) break;
@@ -1523,7 +1463,7 @@ struct rt_renderer {
         // order is unchanged.
         const int nn = sc->bvh_node_count;
         std::vector<int> rec(nn, -1);
-        int nrec = 0, top_recs = 0;
+        int nrec = 0;
         if (nn > 0 && !is_leaf(sc->bvh[0])) {
             rec[0] = 0;
             nrec = 2;                   // record 1: padding, the root has no sibling
@@ -1533,30 +1473,6 @@ struct rt_renderer {
             // run past the per-lane overflow stack, so it is refused here
             std::vector<std::pair<int, int>> todo{{0, 0}};
             int visited = 0;
-            // the top kTopLevels levels first, breadth-first (the trace kernel's LDS copy); their
-            // deepest level's subtrees then depth-first as below
-            for (size_t h = 0; kTopLevels > 1 && h < todo.size(); h++) {
-                const int i = todo[h].first, depth = todo[h].second;
-                if (depth + 1 >= kTopLevels) continue;
-                if (++visited > nn) return rtamd::fail(RT_E_INVALID, "BVH is not a tree");
-                const rt_bvh_node &nd = sc->bvh[i];
-                if (nd.child1 < 0 || nd.child2 >= nn || nd.child1 >= nn || nd.child2 < 0)
-                    return rtamd::fail(RT_E_INVALID, "BVH child index out of range");
-                const bool in1 = !is_leaf(sc->bvh[nd.child1]), in2 = !is_leaf(sc->bvh[nd.child2]);
-                if (in1) rec[nd.child1] = nrec;
-                if (in2) rec[nd.child2] = nrec + 1;
-                if (in1 || in2) nrec += 2;
-                if (in1) todo.push_back({nd.child1, depth + 1});
-                if (in2) todo.push_back({nd.child2, depth + 1});
-                todo[h].first = -1;         // done
-            }
-            top_recs = nrec;
-            if (kTopLevels > 1) {           // the nodes left (the deepest top level) depth-first, in order
-                std::vector<std::pair<int, int>> rest;
-                for (auto it = todo.rbegin(); it != todo.rend(); ++it)
-                    if (it->first >= 0) rest.push_back(*it);
-                todo.swap(rest);
-            }
             while (!todo.empty()) {
                 const int i = todo.back().first, depth = todo.back().second;
                 todo.pop_back();
@@ -1600,7 +1516,6 @@ struct rt_renderer {
             q[3].z = q[3].w = 0.0f;
         }
         ds.root_ref = nn > 0 ? ref_of(0) : (kLeaf | 0u);
-        ds.top_recs = kTopLevels > 0 ? (uint32_t)std::min(top_recs, nrec) : 0u;
         if (big_h.empty()) big_h.push_back(make_int2(0, 0));
         if ((rc = spheres.upload(sc->spheres, sc->sphere_count, s0))) return rc;
         // one float4 of slack: traversal reads 64 B at a triangle record (48 B) like at a node
