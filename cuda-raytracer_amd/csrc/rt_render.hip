@@ -64,9 +64,6 @@ namespace {
 #ifndef RT_QUEUES
 #define RT_QUEUES 8
 #endif
-#ifndef RT_DEFER_SETUP
-#define RT_DEFER_SETUP 0
-#endif
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 constexpr int kStackLds = RT_STACK_LDS; // stack entries per lane kept in LDS (deeper: global)
 constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138)
@@ -121,7 +118,6 @@ constexpr int kStaggerMinPasses = 8;   // ...for renders of at least this many p
 // 100 % (20 in flight: 15 %; A/B at 20 in flight: 40 % 7.51, 30 % 7.41, 20 % 7.37, 15 % 7.33,
 // 10 % 7.35 ms/pass; lamp and the 13-pass share also best at 15 %).
 constexpr int kTraceOccPct = RT_TRACE_OCC;
-constexpr bool kDeferSetup = RT_DEFER_SETUP;   // later bounces: a fresh ray's loads overlap the next step
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
 constexpr int kQueueStride = 64;     // words between shards (256 B: one shard per cache line)
 constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFFFFF)
@@ -457,30 +453,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 #undef RT_U
         rk = make_uint2(__builtin_amdgcn_readfirstlane(k.x), __builtin_amdgcn_readfirstlane(k.y));
     }
-    // A fresh ray's setup (1/d, the sphere loop scene.cu:338-372, the root pop) once o and d are set.
-    auto setup_ray = [&]() {
-        ix = 1 / d.x; iy = 1 / d.y; iz = 1 / d.z;
-        finite_inv = __builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz);
-        closest = 1e30f;
-        index = -1;
-        for (int i = 0; i < S.sphere_count; i++) {
-            const float4 sph = S.spheres[i];
-            float t;
-            if (ray_sphere(o, d, v3(sph.x, sph.y, sph.z), sph.w, closest, t)) { closest = t; index = i; }
-        }
-        ref = S.root_ref;   // root is popped with distance 0 < closest
-        sp = 0;
-        if (COUNT) pn++;
-        ti = te = 0;
-        if (ref & kLeaf) {
-            leaf_range(S, ref, ti, te);
-            if (ti == te) {  // no triangles at all: spheres only
-                hits[slot] = make_float2(closest, __int_as_float(index));
-                slot = -1;
-            }
-        }
-    };
-    bool pending = false;               // kDeferSetup: the lane's ray loads are in flight, set up after the step
     while (true) {
         // ---- refill idle lanes (wave-uniform control flow)
         unsigned long long idle = __ballot(slot < 0);
@@ -519,29 +491,48 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 idle &= ~took;
             }
             if (fresh) {
-                nlive++;
-                if (FIRST) {
-                    o = S.cam;
-                    d = primary_dir(S, (int)first_ray<FIRST>(pa.map, (uint32_t)slot), pa);
-                } else {
-                    const float4 *rp = geo + (size_t)slot * 2;   // ray state is in slot order
-                    const float4 r0 = rp[0];
-                    const float2 r1 = *reinterpret_cast<const float2 *>(rp + 1);
-                    o = v3(r0.x, r0.y, r0.z);
-                    d = v3(r0.w, r1.x, r1.y);
+                {
+                    nlive++;
+                    if (FIRST) {
+                        o = S.cam;
+                        d = primary_dir(S, (int)first_ray<FIRST>(pa.map, (uint32_t)slot), pa);
+                    } else {
+                        const float4 *rp = geo + (size_t)slot * 2;   // ray state is in slot order
+                        const float4 r0 = rp[0];
+                        const float2 r1 = *reinterpret_cast<const float2 *>(rp + 1);
+                        o = v3(r0.x, r0.y, r0.z);
+                        d = v3(r0.w, r1.x, r1.y);
+                    }
+                    ix = 1 / d.x; iy = 1 / d.y; iz = 1 / d.z;
+                    finite_inv = __builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz);
+
+                    closest = 1e30f;
+                    index = -1;
+                    for (int i = 0; i < S.sphere_count; i++) {
+                        const float4 sph = S.spheres[i];
+                        float t;
+                        if (ray_sphere(o, d, v3(sph.x, sph.y, sph.z), sph.w, closest, t)) { closest = t; index = i; }
+                    }
+                    ref = S.root_ref;   // root is popped with distance 0 < closest
+                    sp = 0;
+                    if (COUNT) pn++;
+                    ti = te = 0;
+                    if (ref & kLeaf) {
+                        leaf_range(S, ref, ti, te);
+                        if (ti == te) {  // no triangles at all: spheres only
+                            hits[slot] = make_float2(closest, __int_as_float(index));
+                            slot = -1;
+                        }
+                    }
                 }
-                if (kDeferSetup && !FIRST) pending = true;   // set up after this iteration's step
-                else setup_ray();
             }
             // one ballot per refill instead of one per node step; the flag stays set until the next
             // refill even if that ray has finished (the per-lane fold below is exact for every lane)
-            if (!(kDeferSetup && !FIRST)) {
-                wave_nonfinite = __ballot(slot >= 0 && !finite_inv) != 0;
-                if (root_internal && __ballot(fresh && slot >= 0)) {   // the fresh lanes' root step
-                    bool need = false;
-                    if (fresh && slot >= 0) need = node_step(ra, rb, rc, rk);
-                    pop_loop(need);
-                }
+            wave_nonfinite = __ballot(slot >= 0 && !finite_inv) != 0;
+            if (root_internal && __ballot(fresh && slot >= 0)) {   // the fresh lanes' root step
+                bool need = false;
+                if (fresh && slot >= 0) need = node_step(ra, rb, rc, rk);
+                pop_loop(need);
             }
         }
         if (!__ballot(slot >= 0)) {
@@ -559,9 +550,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             if (mixed) PROF(9, min(__popcll(lf), __popcll(act & ~lf)));
         }
 #endif
-        if (!kDeferSetup && slot < 0) continue;
-        bool need = false;              // the lane needs the next node from its stack
-        if (slot >= 0 && !pending) {
+        if (slot < 0) continue;
         // ---- one step: a single triangle test of the current leaf, or one internal node
         // (both children's slabs).  One triangle per step keeps the leaf branch as short as the
         // internal one, so lanes at leaves and lanes at internal nodes share a step at ~50 %
@@ -570,6 +559,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         // Both kinds of step read their record through the same loads (a triangle's p1 e1 e2, or a
         // node's interleaved child bounds and child refs), issued before the branch, so a step
         // costs one memory round trip whatever mix of leaf and internal lanes the wave holds.
+        bool need = false;              // the lane needs the next node from its stack
         const bool in_leaf = ti < te;
         const float4 *rec = in_leaf ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4;
         const float4 a = rec[0], b = rec[1], c = rec[2];
@@ -586,15 +576,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             need = ++ti == te;
         } else {
             need = node_step(a, b, c, kids);
-        }
-        }
-        if (kDeferSetup && !FIRST && __ballot(pending)) {
-            // the fresh lanes' setup and root step, their ray loads having arrived with the step's
-            // record loads (one memory round trip per refill instead of two)
-            if (pending) setup_ray();
-            wave_nonfinite = __ballot(slot >= 0 && !finite_inv) != 0;
-            if (root_internal && pending && slot >= 0) need = node_step(ra, rb, rc, rk);
-            pending = false;
         }
 #ifdef RT_PROFILE
         if (__ballot(need)) PROF(5, 1);
