@@ -64,9 +64,6 @@ namespace {
 #ifndef RT_QUEUES
 #define RT_QUEUES 8
 #endif
-#ifndef RT_ROOT2_FIRST
-#define RT_ROOT2_FIRST 0
-#endif
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 constexpr int kStackLds = RT_STACK_LDS; // stack entries per lane kept in LDS (deeper: global)
 constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138)
@@ -121,7 +118,6 @@ constexpr int kStaggerMinPasses = 8;   // ...for renders of at least this many p
 // 100 % (20 in flight: 15 %; A/B at 20 in flight: 40 % 7.51, 30 % 7.41, 20 % 7.37, 15 % 7.33,
 // 10 % 7.35 ms/pass; lamp and the 13-pass share also best at 15 %).
 constexpr int kTraceOccPct = RT_TRACE_OCC;
-constexpr bool kRoot2First = RT_ROOT2_FIRST;   // bounce 0: a second (depth-1) step at refill
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
 constexpr int kQueueStride = 64;     // words between shards (256 B: one shard per cache line)
 constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFFFFF)
@@ -325,8 +321,12 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
-    // before its first wave and the stream's marker packets (what rocprofv3 reports)
-    if (tspan && threadIdx.x == 0) atomicMin(&tspan[blockIdx.x % kSpanSlots], (unsigned long long)wall_clock64());
+    // before its first wave and the stream's marker packets (what rocprofv3 reports).  The start is
+    // read into scalar registers here and published with the end at exit: an atomic issued at the
+    // start counts in vmcnt, so the root record's loads below waited for it, and the device-scope
+    // atomics of ~2000 workgroups queue (round 3: 0.76 ms per exclusive teapot launch with the
+    // timing on against 0.63 with it off, both by the profiler's dispatch durations)
+    const unsigned long long t_start = wall_clock64();
     uint2 *col = stack + threadIdx.x;
     // Overflow tail of the stack (entries >= kStackLds, rare) in a global per-lane buffer,
     // [entry][lane] for coalescing; refs and distances in two 32-bit halves so the compiler cannot
@@ -457,24 +457,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 #undef RT_U
         rk = make_uint2(__builtin_amdgcn_readfirstlane(k.x), __builtin_amdgcn_readfirstlane(k.y));
     }
-    // Bounce 0 (RT_ROOT2_FIRST): the root's two children's records too (when both are internal), for
-    // a second step at refill: a refill there hands a whole wave of consecutive primary rays out at once
-    const bool kids_internal = kRoot2First && FIRST && root_internal && !(rk.x & kLeaf) && !(rk.y & kLeaf);
-    float4 xa{0, 0, 0, 0}, xb{0, 0, 0, 0}, xc{0, 0, 0, 0}, ya{0, 0, 0, 0}, yb{0, 0, 0, 0}, yc{0, 0, 0, 0};
-    uint2 xk{0, 0}, yk{0, 0};
-    if (kids_internal) {
-#define RT_U(v) __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)))
-#define RT_U4(v) make_float4(RT_U(v.x), RT_U(v.y), RT_U(v.z), RT_U(v.w))
-        const float4 *px = S.nodes + (size_t)rk.x * 4, *py = S.nodes + (size_t)rk.y * 4;
-        const float4 x0 = px[0], x1 = px[1], x2 = px[2], y0 = py[0], y1 = py[1], y2 = py[2];
-        const uint2 kx = *reinterpret_cast<const uint2 *>(px + 3), ky = *reinterpret_cast<const uint2 *>(py + 3);
-        xa = RT_U4(x0); xb = RT_U4(x1); xc = RT_U4(x2);
-        ya = RT_U4(y0); yb = RT_U4(y1); yc = RT_U4(y2);
-#undef RT_U4
-#undef RT_U
-        xk = make_uint2(__builtin_amdgcn_readfirstlane(kx.x), __builtin_amdgcn_readfirstlane(kx.y));
-        yk = make_uint2(__builtin_amdgcn_readfirstlane(ky.x), __builtin_amdgcn_readfirstlane(ky.y));
-    }
     while (true) {
         // ---- refill idle lanes (wave-uniform control flow)
         unsigned long long idle = __ballot(slot < 0);
@@ -555,15 +537,6 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 bool need = false;
                 if (fresh && slot >= 0) need = node_step(ra, rb, rc, rk);
                 pop_loop(need);
-                const bool on_x = slot >= 0 && !(ti < te) && ref == rk.x, on_y = slot >= 0 && !(ti < te) && ref == rk.y;
-                if (kids_internal && __ballot(on_x || on_y)) {   // any lane about to step a depth-1 node
-                    need = false;
-                    if (on_x || on_y) {
-                        const float4 a = on_x ? xa : ya, b = on_x ? xb : yb, c = on_x ? xc : yc;
-                        need = node_step(a, b, c, on_x ? xk : yk);
-                    }
-                    pop_loop(need);
-                }
             }
         }
         if (!__ballot(slot >= 0)) {
@@ -628,7 +601,10 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     if (lane_id() == 0 && nl) atomicAdd(&cs->live, nl);
     if (tspan) {                        // the workgroup's last wave: one atomic per workgroup
         __syncthreads();
-        if (threadIdx.x == 0) atomicMax(&tspan[kSpanSlots + blockIdx.x % kSpanSlots], (unsigned long long)wall_clock64());
+        if (threadIdx.x == 0) {
+            atomicMin(&tspan[blockIdx.x % kSpanSlots], t_start);
+            atomicMax(&tspan[kSpanSlots + blockIdx.x % kSpanSlots], (unsigned long long)wall_clock64());
+        }
     }
 #ifdef RT_PROFILE
     prof[11] = wave_sum((unsigned)prof[10]);   // pop iterations summed over the lanes
