@@ -6,8 +6,6 @@ import json
 import os
 import sys
 
-import pytest
-
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKLOAD = "teapot.scene 1920x1080 2048spp 16 bounces sort=on"
 
@@ -100,15 +98,6 @@ def test_closing_lines_every_config_bit_exact():
     assert lines["bench_teapot_steps20.json"]["steps"] == 20 and lines["bench_teapot_steps20.json"]["warmup"] == 5
 
 
-def _final_exclusive_is_instrumented():
-    """True while profiles/r03/final/bench_teapot.json comes from a revision whose trace kernel issued its
-    timing atomic at the start (before 'start time published at exit'): with the root step that atomic
-    slowed the timed launches to ~0.76 ms against 0.63 untimed (profiles/r03/root_step/excl_probe/)."""
-    return _final_lines()["bench_teapot.json"]["roofline"]["ms_per_launch"] > 0.74   # the af1f23b line: 0.7466
-
-
-@pytest.mark.xfail(condition=_final_exclusive_is_instrumented(), strict=False,
-                   reason="closing line measured before the timing fix (DESIGN §3); re-measure at HEAD")
 def test_closing_exclusive_launch_agrees_with_the_profiler():
     """The bench's exclusive trace launch duration (device wall clock, one atomic per workgroup) and the
     profiler's average dispatch duration of the same launches agree within 10 %."""
