@@ -127,12 +127,18 @@ struct RunGuard {
         arrived = true;
         return sy.setup_done(true);
     }
-    ~RunGuard() {
-        if (!arrived) (void)sy.setup_done(false);
-        else if (!ok) {
+    // an error after setup: raise the flag and abort this device's communicator now, before the
+    // renderer and buffers are torn down (their teardown must not wait on a collective a peer is
+    // still blocked in); called by the resource guards' destructors, and again (a no-op) at scope exit
+    void fail_now() {
+        if (arrived && !ok) {
             sy.failed = true;
             ln.abort();
         }
+    }
+    ~RunGuard() {
+        if (!arrived) (void)sy.setup_done(false);
+        else fail_now();
     }
 };
 
@@ -206,15 +212,17 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
     if (rc) return rc;
     struct Guard {
         rt_renderer *r;
+        RunGuard &run;
         float *bufs[3] = {nullptr, nullptr, nullptr};
         hipStream_t s = nullptr;
         ~Guard() {
+            run.fail_now();
             for (float *b : bufs)
                 if (b) (void)hipFree(b);
             if (s) (void)hipStreamDestroy(s);
             rt_renderer_destroy(r);
         }
-    } g{ren};
+    } g{ren, run};
     float *&buf = g.bufs[0], *&recv = g.bufs[1], *&slice = g.bufs[2];
     MHIP(hipMalloc(reinterpret_cast<void **>(&buf), (size_t)chunk * pitch * sizeof(float)));
     MHIP(hipMalloc(reinterpret_cast<void **>(&recv), (size_t)chunk * pitch * sizeof(float)));
@@ -311,14 +319,16 @@ int run_device_tiles(const rt_scene *scene, const rt_opts *base, Link &ln, int w
     if (rc) return rc;
     struct Guard {
         rt_renderer *r;
+        RunGuard &run;
         float *d = nullptr;
         hipStream_t s = nullptr;
         ~Guard() {
+            run.fail_now();
             if (d) (void)hipFree(d);
             if (s) (void)hipStreamDestroy(s);
             rt_renderer_destroy(r);
         }
-    } g{ren};
+    } g{ren, run};
     if (o.sort && world > 1) {
         rc = rt_renderer_set_exchange(ren, nccl_exchange, &ln, 1);
         if (rc) return rc;

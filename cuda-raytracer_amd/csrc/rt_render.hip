@@ -284,6 +284,45 @@ __device__ __forceinline__ bool ray_triangle_flat(V3 o, V3 d, V3 p1, V3 e1, V3 e
     return ok_a & ok_u & ok_v & ok_t;
 }
 
+// The closest-independent part of ray_triangle_flat: the hit's t and whether a, u, v accept it.
+// The caller applies the t test (!(t < kEps || t >= closest)) later, against the closest of that
+// moment, so the outcome is ray_triangle_flat's bit for bit.
+__device__ __forceinline__ bool ray_triangle_uv(V3 o, V3 d, V3 p1, V3 e1, V3 e2, float &t) {
+    const V3 h = cross(d, e2);
+    const float a = dot(h, e1);
+    const float f = 1 / a;
+    const V3 s = o - p1;
+    const float u = dot(s, h) * f;
+    const V3 q = cross(s, e1);
+    const float v = dot(d, q) * f;
+    t = dot(e2, q) * f;
+    const bool ok_a = a != 0;
+    const bool ok_u = !(u < 0 || u > 1);
+    const bool ok_v = !(v < 0 || u + v > 1);
+    return ok_a & ok_u & ok_v;
+}
+
+// Wave-wide inclusive scans (DPP row shifts within rows of 16, then the gfx9 row broadcasts;
+// every lane must be active).
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
 // Triangle range [ti, te) of a leaf ref (small leaves inline, big ones through big_leaves).
 __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int &ti, int &te) {
     if (ref & kBigLeaf) {
@@ -312,6 +351,13 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #define RT_SORT_GRID 0                // cap on the reorder's hist/scatter grid (0: 8 blocks per CU)
 #endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8)))
+// Parallel leaves (later bounces): a lane that reaches a leaf waits; once the wave's waiting
+// leaves hold at least RT_LEAFPAR triangles (or no lane has a node step left), their triangles
+// are dealt to all 64 lanes, one triangle test per lane, and each owner merges its leaf's results
+// in triangle order.  0 = off (one triangle per lane and step).
+#ifndef RT_LEAFPAR
+#define RT_LEAFPAR 0
+#endif
 template <bool SORTED, bool COUNT, int FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ live_count,
@@ -319,6 +365,11 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
                                                        unsigned long long *__restrict__ tspan) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
+    constexpr bool kLeafPar = RT_LEAFPAR > 0 && FIRST == 0;
+    // parallel leaves: 64 words per wave, written and read by different lanes of the wave (relaxed
+    // wavefront-scope atomics around a fence: plain ds ops, which the compiler neither forwards from a
+    // lane's own store nor reorders; one wave's LDS operations complete in order)
+    __shared__ uint32_t owner_tab[kLeafPar ? kBlock : 1];
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
     // before its first wave and the stream's marker packets (what rocprofv3 reports).  The start is
@@ -554,6 +605,64 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             if (mixed) PROF(9, min(__popcll(lf), __popcll(act & ~lf)));
         }
 #endif
+        if constexpr (kLeafPar) {
+            // ---- node lanes: one internal node each (a lane standing on a leaf waits)
+            const bool node_lane = slot >= 0 && !(ti < te);
+            if (__ballot(node_lane)) {
+                bool need = false;
+                if (node_lane) {
+                    const float4 *rec = S.nodes + (size_t)ref * 4;
+                    const float4 a = rec[0], b = rec[1], c = rec[2];
+                    const uint2 kids = *reinterpret_cast<const uint2 *>(rec + 3);
+                    need = node_step(a, b, c, kids);
+                }
+                pop_loop(need);
+            }
+            // ---- waiting leaves: their triangles dealt over the wave's lanes in lane order, then
+            // merged by each owner in triangle order (the reference's sequence of closest updates)
+            const uint32_t lane = lane_id();
+            const uint32_t cnt = (slot >= 0 && ti < te) ? (uint32_t)min(te - ti, 64) : 0u;
+            const uint32_t incl = wave_incl_add(cnt);
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            const bool nodes_left = __ballot(slot >= 0 && !(ti < te)) != 0;
+            if (total >= (uint32_t)RT_LEAFPAR || (total && !nodes_left)) {
+                const uint32_t start = incl - cnt;
+                uint32_t *tab = owner_tab + (threadIdx.x & ~63u);
+                __hip_atomic_store(tab + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                if (cnt && start < 64)
+                    __hip_atomic_store(tab + start, lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t own = wave_incl_max(   // owner lane + 1 of triangle position `lane`
+                    __hip_atomic_load(tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
+                const bool worker = lane < total;
+                const int src = worker ? (int)own - 1 : (int)lane;
+                const V3 wo = v3(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
+                const V3 wd = v3(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
+                const int wti = __shfl(ti, src), wst = __shfl((int)start, src);
+                float t = 0;
+                int ok = 0;
+                if (worker) {
+                    const float4 *rec = S.tris + (size_t)(wti + ((int)lane - wst)) * 3;
+                    const float4 q0 = rec[0], q1 = rec[1];
+                    const float q2 = rec[2].x;
+                    ok = ray_triangle_uv(wo, wd, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), t);
+                }
+                const uint32_t ce = (cnt && start < 64) ? min(cnt, 64u - start) : 0u;   // this round's share
+                for (uint32_t k = 0; __ballot(k < ce); k++) {
+                    const int from = k < ce ? (int)(start + k) : (int)lane;
+                    const float tk = __shfl(t, from);
+                    const int okk = __shfl(ok, from);
+                    const bool take = k < ce && okk && !(tk < kEps || tk >= closest);
+                    closest = take ? tk : closest;
+                    index = take ? S.sphere_count + ti + (int)k : index;
+                }
+                if (COUNT) tt += ce;
+                ti += (int)ce;
+                pop_loop(ce && ti == te);
+            }
+            continue;
+        }
         if (slot < 0) continue;
         // ---- one step: a single triangle test of the current leaf, or one internal node
         // (both children's slabs).  One triangle per step keeps the leaf branch as short as the
@@ -1374,6 +1483,9 @@ struct rt_renderer {
     DevBuf<Counters> ctr;
     DevBuf<unsigned long long> tspans;   // per run: [pass][bounce] trace-launch wall-clock spans (event timing on)
     int wall_khz = 0;                    // device wall clock rate (wall_clock64 ticks per ms)
+    // rt_renderer_launch_profile: the last event-timed run's first pass, per bounce
+    std::vector<double> launch_ms;
+    std::vector<uint32_t> launch_live;
     // staggered start of the first passes in flight (run); RTAMD_STAGGER_US overrides, 0 = off
     // the reorder's bucket histogram counted inside the shade kernel (RTAMD_SHADE_HIST=0: its own launch)
     bool shade_hist = !std::getenv("RTAMD_SHADE_HIST") || std::atoi(std::getenv("RTAMD_SHADE_HIST")) != 0;
@@ -1391,9 +1503,12 @@ struct rt_renderer {
     ~rt_renderer() {
         if (xcomm) {
             (void)hipSetDevice(device);
+            // after a failed run, collectives may be pending that a dead peer never joins: abort the
+            // communicator first (that ends them), and only then drain the streams
+            if (failed) (void)ncclCommAbort(static_cast<ncclComm_t>(xcomm));
             for (auto &c : ctx)
                 if (c.stream) (void)hipStreamSynchronize(c.stream);
-            (void)ncclCommDestroy(static_cast<ncclComm_t>(xcomm));
+            if (!failed) (void)ncclCommDestroy(static_cast<ncclComm_t>(xcomm));
         }
         if (xhost) (void)hipHostFree(xhost);
         if (t_begin) (void)hipEventDestroy(t_begin);
@@ -1412,6 +1527,7 @@ struct rt_renderer {
     void *xpoll_user = nullptr;
     // RCCL communicator owned by this renderer (rt_renderer_set_exchange_rccl), or null
     void *xcomm = nullptr;
+    DevBuf<int32_t> sched;            // the schedule check of a run over xcomm (4 ints)
     bool tsort() const { return tile_count > 1 && sort; }
     int pass_count() const { return (spp + 19) / 20; }
     bool tiled() const { return tile_count > 1; }
@@ -1993,7 +2109,26 @@ struct rt_renderer {
     // Passes pass_begin + k*stride, k < count, nctx at a time on separate streams; the
     // framebuffer adds stay in pass order through cross-stream events.
     // pitch: floats between consecutive passes' sums in pass_sums (0 = W*H*3)
+    // A run that failed (or was aborted because a peer device failed) may leave collectives of this
+    // renderer's communicator pending: the destructor then aborts the communicator instead of waiting
+    // for its streams (which could block forever) and destroying it.
+    bool failed = false;
     int run(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st, size_t pitch = 0) {
+        const int rc = run_impl(pass_begin, count, stride, pass_sums, st, pitch);
+        if (rc) failed = true;
+        return rc;
+    }
+    // Waits for everything queued on c's stream; with an abort poll (multi-device tile renders) the
+    // wait is abortable, as wait_event's: a peer that failed never finishes its side of a collective.
+    int wait_stream(PassCtx &c) {
+        if (!xpoll) {
+            HIPCHK(hipStreamSynchronize(c.stream));
+            return RT_OK;
+        }
+        HIPCHK(hipEventRecord(c.done, c.stream));
+        return wait_event(c.done);
+    }
+    int run_impl(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st, size_t pitch) {
         const auto w0 = std::chrono::high_resolution_clock::now();
         HIPCHK(hipSetDevice(device));
         if (stride < 1) stride = 1;
@@ -2044,6 +2179,24 @@ struct rt_renderer {
             const char *stg = std::getenv("RTAMD_TSTAGGER");
             const bool stagger = !stg || std::atoi(stg) != 0;
             const int nc = std::min(inflight, std::max(count, 1));
+            if (xcomm) {
+                // One process per GPU: the exchange order follows the passes in flight and the stagger,
+                // which environment knobs (RTAMD_INFLIGHT, RTAMD_TSTAGGER) set per process.  Owners on
+                // different schedules would sum bytes of different passes without any byte going
+                // missing, so the schedule is checked once per run: max and -min over the owners.
+                int32_t h[4] = {nc, (int)stagger, -nc, -(int)stagger};
+                if (!sched.p)
+                    if (int rc = sched.alloc(4)) return rc;
+                HIPCHK(hipMemcpyAsync(sched.p, h, sizeof(h), hipMemcpyHostToDevice, ctx[0].stream));
+                const ncclResult_t e = ncclAllReduce(sched.p, sched.p, 4, ncclInt32, ncclMax,
+                                                     static_cast<ncclComm_t>(xcomm), ctx[0].stream);
+                if (e != ncclSuccess) return rtamd::fail(RT_E_HIP, std::string("Error ncclAllReduce ") + ncclGetErrorString(e));
+                HIPCHK(hipMemcpyAsync(h, sched.p, sizeof(h), hipMemcpyDeviceToHost, ctx[0].stream));
+                if (int rc = wait_stream(ctx[0])) return rc;
+                if (h[0] != -h[2] || h[1] != -h[3])
+                    return rtamd::fail(RT_E_INVALID, "pixel tiles with sort on: the owners run different exchange "
+                                                     "schedules (RTAMD_INFLIGHT / RTAMD_TSTAGGER must match on every owner)");
+            }
             for (int j = 0; j < nc; j++) {
                 ctx[j].t_b = -1;
                 HIPCHK(hipMemsetAsync(ctx[j].glive.p + 2, 0, sizeof(uint32_t), ctx[j].stream));   // bad bytes of the run
@@ -2081,7 +2234,7 @@ struct rt_renderer {
             for (int j = 0; j < nc; j++) {
                 uint32_t v = 0;
                 HIPCHK(hipMemcpyAsync(&v, ctx[j].glive.p + 2, sizeof(v), hipMemcpyDeviceToHost, ctx[j].stream));
-                HIPCHK(hipStreamSynchronize(ctx[j].stream));
+                if (int rc = wait_stream(ctx[j])) return rc;
                 bad += v;
             }
             if (bad)
@@ -2121,7 +2274,7 @@ struct rt_renderer {
         }
         HIPCHK(hipEventRecord(t_end, s0));
         const double enq_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
-        HIPCHK(hipStreamSynchronize(s0));
+        if (int rc = wait_event(t_end)) return rc;    // abortable when a peer device can fail
         if (std::getenv("RTAMD_TIMING"))
             std::fprintf(stderr, "rt_renderer run: %d passes enqueued in %.2f ms (host), done at %.2f ms\n", count, enq_ms,
                          std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count());
@@ -2175,6 +2328,8 @@ struct rt_renderer {
             }
             // trace launches: the device wall-clock span from the first wave's start to the last
             // wave's end (the stream's events would add the queueing before the first wave)
+            launch_ms.clear();
+            launch_live.clear();
             if (pass_events && !inline_hits && !tsort() && count > 0) {
                 std::vector<unsigned long long> sp((size_t)count * kSpanWords * (bounces + 1));
                 HIPCHK(hipMemcpy(sp.data(), tspans.p, sp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -2190,7 +2345,14 @@ struct rt_renderer {
                             trc += (double)(t1 - t0) / wall_khz;
                             trace_launches++;
                         }
+                        if (k == 0) launch_ms.push_back(t1 >= t0 && t0 != ~0ull ? (double)(t1 - t0) / wall_khz : 0.0);
                     }
+                // live rays per bounce of the first pass: its context's live counts (valid when that
+                // pass was the context's last, i.e. runs of at most `inflight` passes)
+                launch_live.resize((size_t)bounces + 1);
+                HIPCHK(hipMemcpy(launch_live.data(), ctx[0].live.p, launch_live.size() * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost));
+                launch_live.resize((size_t)bounces);
             }
             st->process_ms = proc;
             st->sort_ms = srt;
@@ -2366,6 +2528,16 @@ int rt_renderer_set_event_timing(rt_renderer *r, int32_t enable) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
     r->pass_events = enable != 0;
     return RT_OK;
+}
+
+int rt_renderer_launch_profile(rt_renderer *r, int32_t cap, double *trace_ms_out, uint32_t *live_out) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    const int n = (int)std::min<size_t>(r->launch_ms.size(), (size_t)std::max(cap, 0));
+    for (int b = 0; b < n; b++) {
+        if (trace_ms_out) trace_ms_out[b] = r->launch_ms[b];
+        if (live_out) live_out[b] = b < (int)r->launch_live.size() ? r->launch_live[b] : 0u;
+    }
+    return n;
 }
 
 int rt_renderer_set_exchange(rt_renderer *r, rt_exchange_fn fn, void *user, int32_t on_device) {

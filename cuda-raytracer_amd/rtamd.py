@@ -341,6 +341,18 @@ class Renderer:
     def set_counters(self, on):
         _check(lib().rt_renderer_set_counters(self.h, int(on)))
 
+    def launch_profile(self, cap=256):
+        """Per trace launch of the last event-timed run's first pass: [(span ms, live rays), ...]
+        (rt_renderer_launch_profile)."""
+        f = lib().rt_renderer_launch_profile
+        f.argtypes = [P, I32, P, P]
+        ms = np.zeros(cap, np.float64)
+        live = np.zeros(cap, np.uint32)
+        n = f(self.h, cap, _ptr(ms), _ptr(live))
+        if n < 0:
+            _check(n)
+        return [(float(ms[b]), int(live[b])) for b in range(n)]
+
     def set_event_timing(self, on):
         """Per-bounce HIP events for process_ms / sort_ms (default on; off is ~2 % faster)."""
         f = lib().rt_renderer_set_event_timing

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 enum {
     RT_OK = 0,
@@ -209,6 +209,13 @@ int rt_renderer_set_counters(rt_renderer *r, int32_t enable);
 /* Per-bounce HIP events behind rt_stats.process_ms / sort_ms (default on).  Off, those stay 0 and
  * a pass's stream carries no marker packets between its kernels (~2 % faster frames). */
 int rt_renderer_set_event_timing(rt_renderer *r, int32_t enable);
+/* Per trace launch of the last run's first pass (event timing on): trace_ms_out[b] = the launch's
+ * device wall-clock span (first wave start to last wave end) and live_out[b] = the live rays it
+ * traced, for bounce b < cap.  Returns the number of launches written (0 without event timing or
+ * for scenes without triangles).  Live counts are that pass's when it was the last pass of its
+ * context (runs of at most as many passes as are in flight: the benchmark's one-pass exclusive
+ * run).  Measurement only; no reference counterpart. */
+int rt_renderer_launch_profile(rt_renderer *r, int32_t cap, double *trace_ms_out, uint32_t *live_out);
 void rt_renderer_destroy(rt_renderer *r);
 
 /* Closest hit of n caller rays: rays = n x {o.x o.y o.z d.x d.y d.z} (d unit length, as every

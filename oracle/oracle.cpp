@@ -27,6 +27,15 @@
 #ifdef _OPENMP
 #include <omp.h>
 #endif
+#ifdef ORC_FASTMATH
+#include <pmmintrin.h>
+#include <xmmintrin.h>
+// FTZ/DAZ (nvcc -ftz=true) for the loading thread; the study renders with one thread
+__attribute__((constructor)) static void orc_fastmath_ftz() {
+    _MM_SET_FLUSH_ZERO_MODE(_MM_FLUSH_ZERO_ON);
+    _MM_SET_DENORMALS_ZERO_MODE(_MM_DENORMALS_ZERO_ON);
+}
+#endif
 
 namespace {
 
@@ -48,7 +57,27 @@ inline V3 cross(V3 a, V3 b) {                                                   
     return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
 inline float magsq(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }                  // :82
-inline V3 normalise(V3 v) { return (1.0f / sqrtf(magsq(v))) * v; }                      // :111
+// The fast-math study build (oracle/Makefile: build/liboracle_fastmath.so, -DORC_FASTMATH with
+// -ffp-contract=fast -mfma) perturbs the restatement the way nvcc --use_fast_math (build.sh:2) moves
+// the reference's GPU path away from IEEE arithmetic: FMA contraction (-fmad=true), division as a
+// multiply by a float reciprocal (-prec-div=false), sqrt and 1/sqrt through a float reciprocal
+// square root (-prec-sqrt=false, rsqrtf), __sinf/__cosf (argument scaled by 1/(2 pi) in float, the
+// result to 2^-22 absolute: the MUFU's ~2^-21.4 error), and FTZ/DAZ.  It models the size of those
+// deviations, not nvcc's exact bits (tools/fastmath_floor.py: the image error they alone cause).
+// The IEEE build (liboracle.so, parity) expands every macro to the plain operation.
+#ifdef ORC_FASTMATH
+inline float FDIV(float a, float b) { return a * (float)(1.0 / (double)b); }
+inline float FRSQRT(float x) { return (float)(1.0 / std::sqrt((double)x)); }
+inline float FSQRT(float x) {
+    if (!(x > 0) || std::isinf(x)) return sqrtf(x);
+    return x * FRSQRT(x);
+}
+#else
+#define FDIV(a, b) ((a) / (b))
+#define FRSQRT(x) (1.0f / sqrtf(x))
+#define FSQRT(x) sqrtf(x)
+#endif
+inline V3 normalise(V3 v) { return FRSQRT(magsq(v)) * v; }                              // :111
 inline float clamp01(float x) { return fmax_(fmin_(x, 1.0f), 0.0f); }                   // :116-124
 inline V3 vmin(V3 a, V3 b) { return {fmin_(a.x, b.x), fmin_(a.y, b.y), fmin_(a.z, b.z)}; }
 inline V3 vmax(V3 a, V3 b) { return {fmax_(a.x, b.x), fmax_(a.y, b.y), fmax_(a.z, b.z)}; }
@@ -74,6 +103,13 @@ inline void rt_sincos(float x, float *s, float *c) {
     default: *s = -cp; *c = sp; break;
     }
 }
+#ifdef ORC_FASTMATH
+inline void fm_sincos(float x, float *s, float *c) {     // __sinf / __cosf (MUFU) stand-in
+    const double t = (double)(x * 0.159154943f) * 6.283185307179586;
+    *s = (float)(std::nearbyint(std::sin(t) * 4194304.0) / 4194304.0);
+    *c = (float)(std::nearbyint(std::cos(t) * 4194304.0) / 4194304.0);
+}
+#endif
 inline float rt_atan01(float x) {
     float y = 0.0f;
     if (x > 0.4142135623730950f) { y = 0.78539816339744830962f; x = (x - 1.0f) / (x + 1.0f); }
@@ -104,9 +140,13 @@ inline float random_radians(Rng *r) {                                           
 inline V3 random_on_sphere(Rng *r) {                                                   // :63-75
     const float r1 = random_radians(r);
     const float r2 = random02(r);
-    const float x = sqrtf(r2 * (2 - r2));
+    const float x = FSQRT(r2 * (2 - r2));
     float s, c;
+#ifdef ORC_FASTMATH
+    fm_sincos(r1, &s, &c);
+#else
     rt_sincos(r1, &s, &c);
+#endif
     return {c * x, s * x, 1 - r2};
 }
 
@@ -479,7 +519,7 @@ inline bool ray_tri(const Triangle &tr, V3 o, V3 d, float closest, float *t_out)
     const V3 h = cross(d, tr.p3p1);
     const float a = dot(h, tr.p2p1);
     if (a == 0) return false;
-    const float f = 1 / a;
+    const float f = FDIV(1.0f, a);
     const V3 s = o - tr.p1;
     const float u = dot(s, h) * f;
     if (u < 0 || u > 1) return false;
@@ -499,7 +539,7 @@ inline bool ray_sphere(const Sphere &sp, V3 o, V3 d, float closest, float *t_out
     const float qc = magsq(off) - sp.radius * sp.radius;
     const float qd = mhb * mhb - qc;
     if (qd < 0) return false;
-    const float hs = sqrtf(qd);
+    const float hs = FSQRT(qd);
     float t = mhb - hs;
     if (t < closest && !below_eps(t)) { *t_out = t; return true; }
     t = mhb + hs;
@@ -521,7 +561,7 @@ struct Counters {
 
 // ---------------------------------------------------------------- scene.cu:134-241
 void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index, Counters &c) {
-    const V3 n_inv{1 / d.x, 1 / d.y, 1 / d.z};
+    const V3 n_inv{FDIV(1.0f, d.x), FDIV(1.0f, d.y), FDIV(1.0f, d.z)};
     uint32_t idx_stack[31];
     float dist_stack[31];
     int sc = 1;
@@ -569,10 +609,10 @@ void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index,
 // ---------------------------------------------------------------- scene.cu:284-318
 V3 equal_area_project(V3 dir) {
     const float x = std::fabs(dir.x), y = std::fabs(dir.y), z = std::fabs(dir.z);
-    const float r = sqrtf(1 - fmin_(z, 1.0f));
+    const float r = FSQRT(1 - fmin_(z, 1.0f));
     const float a = fmax_(x, y);
     float b = fmin_(x, y);
-    b = a == 0 ? 0 : b / a;
+    b = a == 0 ? 0 : FDIV(b, a);
     float phi = (float)((2 / 3.14159265358979323846) * (double)rt_atan01(b));
     if (x < y) phi = 1 - phi;
     float v = phi * r;
@@ -633,7 +673,7 @@ void process_ray(const orc_scene *s, RayData *rp, uint32_t *key, Rng rng, bool g
         if (index < sphere_count) {
             c.hs++;
             const Sphere &sp = s->spheres[index];
-            normal = (1 / sp.radius) * (hit - sp.center);
+            normal = FDIV(1.0f, sp.radius) * (hit - sp.center);
         } else {
             c.ht++;
             normal = s->triangles[index - sphere_count].normal;
@@ -654,10 +694,10 @@ void process_ray(const orc_scene *s, RayData *rp, uint32_t *key, Rng rng, bool g
             }
         } else {
             float ior = m.ior;
-            float inv_ior = 1 / ior;
+            float inv_ior = FDIV(1.0f, ior);
             if (front) std::swap(ior, inv_ior);
             const float sin2 = 1 - cos_theta * cos_theta;
-            float r0 = (1 - ior) / (1 + ior);
+            float r0 = FDIV(1 - ior, 1 + ior);
             r0 *= r0;
             const float cs = 1 + cos_theta;
             const float refl = r0 + (1 - r0) * cs * cs * cs * cs * cs;
@@ -667,7 +707,7 @@ void process_ray(const orc_scene *s, RayData *rp, uint32_t *key, Rng rng, bool g
             } else {
                 rd.transmitted = rd.transmitted * m.diffuse;
                 const V3 perp = ior * (d - cos_theta * rough);
-                const V3 par = (-sqrtf(1 - magsq(perp))) * rough;
+                const V3 par = (-FSQRT(1 - magsq(perp))) * rough;
                 rd.dir = normalise(par + perp);
             }
         }

@@ -7,7 +7,8 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
-LIB_PATH = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+# ORACLE_LIB: another build of the oracle (tools/fastmath_floor.py: build/liboracle_fastmath.so)
+LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(ORACLE_DIR, "build", "liboracle.so")
 ASSETS = os.path.join(REPO, "assets")
 
 

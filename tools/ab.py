@@ -38,10 +38,10 @@ def main():
                 print("variant %s failed rc=%d: %s" % (n, out.returncode, out.stderr[-2000:]), flush=True)
                 sys.exit(1)
             rec = json.loads(out.stdout.strip().splitlines()[-1])
-            res[n].append((rec["ms_per_step"], rec["config"]["process_ms_per_step"], rec["value"]))
+            spans = rec["config"].get("summed_concurrent_spans_per_pass", {})
+            res[n].append((rec["ms_per_step"], spans.get("process_ms", 0.0), rec["value"]))
             print("round %d %-12s ms/step %.3f process %.3f Mrays/s %.1f trace/step %s sort/step %s" % (
-                r, n, *res[n][-1], rec["config"].get("trace_ms_per_step"), rec["config"].get("sort_ms_per_step")),
-                flush=True)
+                r, n, *res[n][-1], spans.get("trace_ms"), spans.get("sort_ms")), flush=True)
     print("summary (median / min ms_per_step, median process ms, median Mrays/s):")
     for n in names:
         ms = [x[0] for x in res[n]]
