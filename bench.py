@@ -381,6 +381,25 @@ class RtamdBackend:
         fb0, _ = rtamd.render(scene, sort=sort, device=self.local, pass_begin=0, pass_count=1)
         return fb0
 
+    def async_render(self, ren, on_stats):
+        """The renderer's asynchronous form for rtamd_dist.PassShardedFrame: the slices of finished passes
+        are exchanged while later passes render (RTAMD_XCHG_OVERLAP=0: one exchange after the batch)."""
+        if os.environ.get("RTAMD_XCHG_OVERLAP", "1") == "0":
+            return None
+        torch = self.torch
+
+        class AsyncPasses:
+            def start(self, passes, out):
+                stride = passes[1] - passes[0] if len(passes) > 1 else 1
+                ren.run_async(passes[0], len(passes), stride, out.data_ptr())
+
+            def wait(self, j):
+                ren.wait_pass(j, torch.cuda.current_stream().cuda_stream)
+
+            def finish(self):
+                on_stats(ren.finish())
+        return AsyncPasses()
+
     def barrier_sync(self):
         if self.use_dist:
             self.dist.barrier()
@@ -475,7 +494,9 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
             frame = rtamd_dist.TileShardedFrame(dist, torch, W, H, backend.device,
                                                 lambda out: ren.copy_framebuffer(out.data_ptr()), rows=TILE_ROWS)
         else:
-            frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, backend.device, render_passes)
+            async_render = backend.async_render(ren, accumulate_stats) if hasattr(backend, "async_render") else None
+            frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, backend.device, render_passes,
+                                                async_render=async_render)
 
     def run_steps(k, stats):
         """k steps from the first pass of the frame, wrapping at its end; one pass per GPU per

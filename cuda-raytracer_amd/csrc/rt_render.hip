@@ -350,22 +350,33 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #ifndef RT_SORT_GRID
 #define RT_SORT_GRID 0                // cap on the reorder's hist/scatter grid (0: 8 blocks per CU)
 #endif
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8)))
-// Parallel leaves (later bounces): a lane that reaches a leaf waits; once the wave's waiting
-// leaves hold at least RT_LEAFPAR triangles (or no lane has a node step left), their triangles
-// are dealt to all 64 lanes, one triangle test per lane, and each owner merges its leaf's results
-// in triangle order.  0 = off (one triangle per lane and step).
+// Parallel leaves (later bounces): a lane that reaches a leaf waits; once RT_LEAFPAR lanes of the
+// wave wait (or no lane has a node step left), their leaves' triangles are dealt to all 64 lanes,
+// one triangle test per lane, and each owner merges its leaf's results in triangle order.  0 = off
+// (one triangle per lane and step).
 #ifndef RT_LEAFPAR
 #define RT_LEAFPAR 0
 #endif
-template <bool SORTED, bool COUNT, int FIRST>
-__global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
+// Later-bounce kernels may ask for fewer waves per SIMD as the minimum (RT_TRACE_WPE_LATER 7: the
+// allocator then still lands at <= 64 VGPRs, 8 waves, but without the SGPR spills to VGPR lanes it
+// makes under a hard 8); the bounce-0 kernels keep RT_TRACE_WPE.
+#ifndef RT_TRACE_WPE_LATER
+#define RT_TRACE_WPE_LATER RT_TRACE_WPE
+#endif
+#ifndef RT_LEAFPAR_WPE
+#define RT_LEAFPAR_WPE 7
+#endif
+template <bool SORTED, bool COUNT, int FIRST, bool LEAF = false>
+__global__ __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu((LEAF && FIRST == 0 && RT_LEAFPAR > 0) ? RT_LEAFPAR_WPE
+                                   : (FIRST == 0 ? RT_TRACE_WPE_LATER : RT_TRACE_WPE),
+                                   RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8))) void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
                                                        unsigned long long *__restrict__ tspan) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
-    constexpr bool kLeafPar = RT_LEAFPAR > 0 && FIRST == 0;
+    constexpr bool kLeafPar = RT_LEAFPAR > 0 && FIRST == 0 && LEAF;
     // parallel leaves: 64 words per wave, written and read by different lanes of the wave (relaxed
     // wavefront-scope atomics around a fence: plain ds ops, which the compiler neither forwards from a
     // lane's own store nor reorders; one wave's LDS operations complete in order)
@@ -606,27 +617,32 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         }
 #endif
         if constexpr (kLeafPar) {
-            // ---- node lanes: one internal node each (a lane standing on a leaf waits)
-            const bool node_lane = slot >= 0 && !(ti < te);
-            if (__ballot(node_lane)) {
-                bool need = false;
-                if (node_lane) {
-                    const float4 *rec = S.nodes + (size_t)ref * 4;
-                    const float4 a = rec[0], b = rec[1], c = rec[2];
-                    const uint2 kids = *reinterpret_cast<const uint2 *>(rec + 3);
-                    need = node_step(a, b, c, kids);
-                }
-                pop_loop(need);
-            }
-            // ---- waiting leaves: their triangles dealt over the wave's lanes in lane order, then
-            // merged by each owner in triangle order (the reference's sequence of closest updates)
+            // One memory round trip per iteration for both kinds of work: the node lanes' records and
+            // (when the leaf phase runs) the dealt triangles are in flight together.
             const uint32_t lane = lane_id();
-            const uint32_t cnt = (slot >= 0 && ti < te) ? (uint32_t)min(te - ti, 64) : 0u;
-            const uint32_t incl = wave_incl_add(cnt);
-            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-            const bool nodes_left = __ballot(slot >= 0 && !(ti < te)) != 0;
-            if (total >= (uint32_t)RT_LEAFPAR || (total && !nodes_left)) {
-                const uint32_t start = incl - cnt;
+            const bool node_lane = slot >= 0 && !(ti < te);
+            const unsigned long long waiting = __ballot(slot >= 0 && ti < te);
+            const bool do_leaf = __popcll(waiting) >= RT_LEAFPAR || (waiting && !__ballot(node_lane));
+            float4 a{0, 0, 0, 0}, b{0, 0, 0, 0}, c{0, 0, 0, 0};
+            uint2 kids{0, 0};
+            if (node_lane) {
+                const float4 *rec = S.nodes + (size_t)ref * 4;
+                a = rec[0]; b = rec[1]; c = rec[2];
+                kids = *reinterpret_cast<const uint2 *>(rec + 3);
+            }
+            // ---- waiting leaves: their triangles dealt over the wave's lanes in lane order (position
+            // p = one triangle), loaded now; tested after the node step, then merged by each owner in
+            // triangle order (the reference's sequence of closest updates)
+            uint32_t cnt = 0, start = 0;
+            int src = (int)lane;
+            bool worker = false;
+            float4 q0{0, 0, 0, 0}, q1{0, 0, 0, 0};
+            float q2 = 0;
+            if (do_leaf) {
+                cnt = (slot >= 0 && ti < te) ? (uint32_t)min(te - ti, 64) : 0u;
+                const uint32_t incl = wave_incl_add(cnt);
+                const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                start = incl - cnt;
                 uint32_t *tab = owner_tab + (threadIdx.x & ~63u);
                 __hip_atomic_store(tab + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
                 if (cnt && start < 64)
@@ -635,27 +651,43 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                 __builtin_amdgcn_wave_barrier();
                 const uint32_t own = wave_incl_max(   // owner lane + 1 of triangle position `lane`
                     __hip_atomic_load(tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
-                const bool worker = lane < total;
-                const int src = worker ? (int)own - 1 : (int)lane;
+                worker = lane < total;
+                src = worker ? (int)own - 1 : (int)lane;
+                const int base = __shfl(ti - (int)start, src);   // triangle of position p = base + p
+                if (worker) {
+                    const float4 *rec = S.tris + (size_t)(base + (int)lane) * 3;
+                    q0 = rec[0]; q1 = rec[1]; q2 = rec[2].x;
+                }
+            }
+            // ---- node lanes: one internal node each (a lane standing on a leaf waits)
+            if (__ballot(node_lane)) {
+                bool need = false;
+                if (node_lane) need = node_step(a, b, c, kids);
+                pop_loop(need);
+            }
+            if (do_leaf) {
+                // the owners' rays (unchanged by the node step: an owner was not a node lane)
                 const V3 wo = v3(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
                 const V3 wd = v3(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
-                const int wti = __shfl(ti, src), wst = __shfl((int)start, src);
-                float t = 0;
-                int ok = 0;
+                // t where a, u and v accept the hit, else -1 (which the t test rejects as the
+                // reference's early-outs do); a NaN t stays NaN and is accepted as in the reference
+                float tv = -1.0f;
                 if (worker) {
-                    const float4 *rec = S.tris + (size_t)(wti + ((int)lane - wst)) * 3;
-                    const float4 q0 = rec[0], q1 = rec[1];
-                    const float q2 = rec[2].x;
-                    ok = ray_triangle_uv(wo, wd, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), t);
+                    float t;
+                    tv = ray_triangle_uv(wo, wd, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), t)
+                             ? t : -1.0f;
                 }
                 const uint32_t ce = (cnt && start < 64) ? min(cnt, 64u - start) : 0u;   // this round's share
-                for (uint32_t k = 0; __ballot(k < ce); k++) {
-                    const int from = k < ce ? (int)(start + k) : (int)lane;
-                    const float tk = __shfl(t, from);
-                    const int okk = __shfl(ok, from);
-                    const bool take = k < ce && okk && !(tk < kEps || tk >= closest);
-                    closest = take ? tk : closest;
-                    index = take ? S.sphere_count + ti + (int)k : index;
+                for (uint32_t k0 = 0; __ballot(k0 < ce); k0 += 4) {   // four positions' results per exchange
+                    float tk[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) tk[j] = __shfl(tv, k0 + j < ce ? (int)(start + k0 + j) : (int)lane);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const bool take = k0 + j < ce && !(tk[j] < kEps || tk[j] >= closest);
+                        closest = take ? tk[j] : closest;
+                        index = take ? S.sphere_count + ti + (int)(k0 + j) : index;
+                    }
                 }
                 if (COUNT) tt += ce;
                 ti += (int)ce;
@@ -1483,6 +1515,8 @@ struct rt_renderer {
     DevBuf<Counters> ctr;
     DevBuf<unsigned long long> tspans;   // per run: [pass][bounce] trace-launch wall-clock spans (event timing on)
     int wall_khz = 0;                    // device wall clock rate (wall_clock64 ticks per ms)
+    // parallel-leaf trace (RT_LEAFPAR builds) from this bounce on (RTAMD_LEAFPAR_FROM, default 1)
+    int leafpar_from = std::getenv("RTAMD_LEAFPAR_FROM") ? std::atoi(std::getenv("RTAMD_LEAFPAR_FROM")) : 1;
     // rt_renderer_launch_profile: the last event-timed run's first pass, per bounce
     std::vector<double> launch_ms;
     std::vector<uint32_t> launch_live;
@@ -1501,6 +1535,9 @@ struct rt_renderer {
     hipEvent_t t_begin = nullptr, t_end = nullptr;
 
     ~rt_renderer() {
+        (void)hipSetDevice(device);
+        if (run_pending && t_end) (void)hipEventSynchronize(t_end);   // an async run never finished
+        for (hipEvent_t e : pass_done) (void)hipEventDestroy(e);
         if (xcomm) {
             (void)hipSetDevice(device);
             // after a failed run, collectives may be pending that a dead peer never joins: abort the
@@ -1789,7 +1826,11 @@ struct rt_renderer {
             uint32_t *hist = shade_hist && !last ? c.sort_counts.p : nullptr;   // the shade kernel counts the buckets
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
-        if (!inline_hits)                                                                                        \
+        if (!inline_hits && RT_LEAFPAR > 0 && FIRST == 0 && b >= leafpar_from)                                   \
+            hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST, true>), dim3(tgrid), dim3(kBlock), 0, st, ds, \
+                               pa, c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p,                          \
+                               tspan ? tspan + kSpanWords * b : nullptr);                                        \
+        else if (!inline_hits)                                                                                   \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
                                c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr); \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
@@ -2114,7 +2155,24 @@ struct rt_renderer {
     // for its streams (which could block forever) and destroying it.
     bool failed = false;
     int run(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st, size_t pitch = 0) {
-        const int rc = run_impl(pass_begin, count, stride, pass_sums, st, pitch);
+        int rc = run_impl(pass_begin, count, stride, pass_sums, st, pitch, false);
+        if (!rc) rc = finish_run(st);
+        if (rc) failed = true;
+        return rc;
+    }
+    // rt_renderer_run_async: the same passes enqueued, nothing waited for; pass k's sums are complete at
+    // pass_done[k] (rt_renderer_wait_pass), the run at finish_run (rt_renderer_finish)
+    bool run_pending = false;
+    int run_count = 0, run_inflight = 0;
+    int64_t run_sorted = 0, run_generated = 0;
+    std::chrono::high_resolution_clock::time_point run_w0;
+    double run_enq_ms = 0;
+    std::vector<hipEvent_t> pass_done;
+    int run_async(int pass_begin, int count, int stride, float *pass_sums) {
+        if (run_pending) return rtamd::fail(RT_E_INVALID, "rt_renderer_run_async: the previous run is not finished");
+        if (!pass_sums) return rtamd::fail(RT_E_INVALID, "rt_renderer_run_async: the pass sums buffer is required");
+        if (tsort()) return rtamd::fail(RT_E_INVALID, "rt_renderer_run_async: not for pixel tiles with sort on");
+        const int rc = run_impl(pass_begin, count, stride, pass_sums, nullptr, 0, true);
         if (rc) failed = true;
         return rc;
     }
@@ -2128,7 +2186,7 @@ struct rt_renderer {
         HIPCHK(hipEventRecord(c.done, c.stream));
         return wait_event(c.done);
     }
-    int run_impl(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st, size_t pitch) {
+    int run_impl(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st, size_t pitch, bool async) {
         const auto w0 = std::chrono::high_resolution_clock::now();
         HIPCHK(hipSetDevice(device));
         if (stride < 1) stride = 1;
@@ -2265,6 +2323,14 @@ struct rt_renderer {
                 const int rc = enqueue_pass(c, p, sums, sorted,
                                             pass_events ? tspans.p + (size_t)k * kSpanWords * (bounces + 1) : nullptr);
                 if (rc) return rc;
+                if (async) {                    // pass k's sums are written: what a caller's stream may wait for
+                    while ((int)pass_done.size() <= k) {
+                        hipEvent_t e;
+                        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                        pass_done.push_back(e);
+                    }
+                    HIPCHK(hipEventRecord(pass_done[k], c.stream));
+                }
                 if (int rc2 = add_pass(c, p, sums)) return rc2;
             }
         }
@@ -2273,10 +2339,27 @@ struct rt_renderer {
             HIPCHK(hipStreamWaitEvent(s0, ctx[k].done, 0));
         }
         HIPCHK(hipEventRecord(t_end, s0));
-        const double enq_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
+        run_enq_ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count();
+        run_pending = true;
+        run_count = count;
+        run_inflight = inflight;
+        run_sorted = sorted;
+        run_generated = generated;
+        run_w0 = w0;
+        (void)async;
+        return RT_OK;
+    }
+    // Waits for the run enqueued last and fills `st` (rt_renderer_run, rt_renderer_finish).
+    int finish_run(rt_stats *st) {
+        if (!run_pending) return rtamd::fail(RT_E_INVALID, "rt_renderer_finish: no run in flight");
+        run_pending = false;
+        HIPCHK(hipSetDevice(device));
+        const int count = run_count, inflight = run_inflight;
+        const int64_t sorted = run_sorted, generated = run_generated;
+        const auto w0 = run_w0;
         if (int rc = wait_event(t_end)) return rc;    // abortable when a peer device can fail
         if (std::getenv("RTAMD_TIMING"))
-            std::fprintf(stderr, "rt_renderer run: %d passes enqueued in %.2f ms (host), done at %.2f ms\n", count, enq_ms,
+            std::fprintf(stderr, "rt_renderer run: %d passes enqueued in %.2f ms (host), done at %.2f ms\n", count, run_enq_ms,
                          std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count());
 #ifdef RT_PROFILE
         {
@@ -2528,6 +2611,27 @@ int rt_renderer_set_event_timing(rt_renderer *r, int32_t enable) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
     r->pass_events = enable != 0;
     return RT_OK;
+}
+
+int rt_renderer_run_async(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride, float *d_pass_sums) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    return r->run_async(pass_begin, count, stride, d_pass_sums);
+}
+
+int rt_renderer_wait_pass(rt_renderer *r, int32_t k, void *hip_stream) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    if (!r->run_pending || k < 0 || k >= r->run_count || k >= (int)r->pass_done.size())
+        return rtamd::fail(RT_E_INVALID, "rt_renderer_wait_pass: no such pass in the async run");
+    HIPCHK(hipSetDevice(r->device));
+    HIPCHK(hipStreamWaitEvent(static_cast<hipStream_t>(hip_stream), r->pass_done[k], 0));
+    return RT_OK;
+}
+
+int rt_renderer_finish(rt_renderer *r, rt_stats *stats) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    const int rc = r->finish_run(stats);
+    if (rc) r->failed = true;
+    return rc;
 }
 
 int rt_renderer_launch_profile(rt_renderer *r, int32_t cap, double *trace_ms_out, uint32_t *live_out) {

@@ -299,6 +299,26 @@ class Renderer:
                                      P(d_pass_sums) if d_pass_sums else None, C.byref(st)))
         return st.as_dict()
 
+    def run_async(self, pass_begin=0, count=1, stride=1, d_pass_sums=None):
+        """rt_renderer_run_async: enqueue the passes and return; then wait_pass / finish."""
+        f = lib().rt_renderer_run_async
+        f.argtypes = [P, I32, I32, I32, P]
+        _check(f(self.h, pass_begin, count, stride, P(d_pass_sums) if d_pass_sums else None))
+
+    def wait_pass(self, k, hip_stream):
+        """The HIP stream `hip_stream` (a raw handle, e.g. torch.cuda.current_stream().cuda_stream)
+        waits until pass k of the async run has written its sums."""
+        f = lib().rt_renderer_wait_pass
+        f.argtypes = [P, I32, P]
+        _check(f(self.h, int(k), P(hip_stream) if hip_stream else None))
+
+    def finish(self):
+        st = RtStats()
+        f = lib().rt_renderer_finish
+        f.argtypes = [P, P]
+        _check(f(self.h, C.byref(st)))
+        return st.as_dict()
+
     def run_host(self, pass_begin=0, count=1, stride=1):
         """Renders passes and returns their per-pass sums (count, W*H*3) in host memory."""
         out = np.zeros((count, self.scene.pixels * 3), np.float32)

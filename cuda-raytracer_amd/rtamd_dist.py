@@ -11,7 +11,9 @@ its pass framebuffers to rank j in one all-to-all (RCCL over xGMI: every link ca
 the data, nothing converges on one GPU), and each owner adds the pass slices it received in
 pass order: fb_j = ((0 + S_0,j) + S_1,j) + ... exactly as one GPU adds whole passes, so the
 N-GPU image is bit-identical to the 1-GPU image.  `collect()` gathers the N finished slices to
-rank 0 (one framebuffer, 24.9 MB at 1080p).  There is no per-bounce collective.
+rank 0 (one framebuffer, 24.9 MB at 1080p).  There is no per-bounce collective.  With an
+asynchronous renderer (rtamd.Renderer.run_async) the exchange of each group of rounds overlaps the
+rendering of the later ones: torch's stream waits on the renderer's per-pass events only.
 """
 from typing import Callable, List, Optional
 
@@ -40,7 +42,7 @@ class PassShardedFrame:
     """
 
     def __init__(self, dist, torch, pixels3: int, passes: int, device, render_passes: Callable,
-                 max_rounds_per_call: Optional[int] = None):
+                 max_rounds_per_call: Optional[int] = None, async_render=None, exchange_rounds: int = 4):
         self.dist, self.torch = dist, torch
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
@@ -58,6 +60,13 @@ class PassShardedFrame:
         self.stage = None if self.world * self.sl == pixels3 else \
             torch.zeros((self.chunk, pixels3), dtype=f32, device=device)
         self.fb: Optional[object] = None
+        # Overlapped exchange: async_render.start(passes, out) enqueues the passes and returns,
+        # async_render.wait(j) makes torch's current stream wait until the j-th of them has written its
+        # sums, async_render.finish() waits for the rest.  The slices of every `exchange_rounds` rounds
+        # then go to their owners while later passes still render (rtamd.Renderer.run_async /
+        # wait_pass / finish); without it, one exchange after the chunk's render call.
+        self.async_render = async_render
+        self.xrounds = max(1, exchange_rounds)
 
     def reset(self):
         self.slice.zero_()
@@ -70,34 +79,52 @@ class PassShardedFrame:
     def run_rounds(self, k0: int, nrounds: int) -> int:
         """Rounds k0 .. k0+nrounds-1: rank r renders passes r + N*k (those that exist) in one
         renderer call per chunk; the pass slices go to their owners, which add them in pass
-        order.  Returns the number of passes this rank rendered."""
+        order (with async_render: every `exchange_rounds` rounds, as soon as this rank's passes of
+        those rounds are done, while its later passes render).  Returns the number of passes this
+        rank rendered."""
         done = 0
         N, sl = self.world, self.sl
         for c0 in range(k0, k0 + nrounds, self.chunk):
             ks = list(range(c0, min(c0 + self.chunk, k0 + nrounds)))
             m = len(ks)
+            # this rank's passes of those rounds: a prefix of them (pass rank + N*k exists up to some k),
+            # so the j-th of `mine` is round ks[j]'s
             mine = [self.rank + N * k for k in ks if self.rank + N * k < self.passes]
+            out = self.buf if self.stage is None else self.stage
             if mine:
                 # The renderer writes the pass sums on its own streams, which do not wait for torch's:
                 # torch work queued earlier that still reads these buffers (the last chunk's
                 # all_to_all send copy, the stage -> buf copy) must finish first.
                 self._sync()
-                if self.stage is None:
-                    self.render_passes(mine, self.buf[:len(mine)])
+                if self.async_render is not None:
+                    self.async_render.start(mine, out[:len(mine)])
                 else:
-                    self.render_passes(mine, self.stage[:len(mine)])
-                    self.buf[:len(mine), :self.pixels3].copy_(self.stage[:len(mine)])
-            if N > 1:
-                # send[d, j] = slice d of this rank's pass framebuffer of round ks[j]
-                send = self.buf[:m].view(m, N, sl).transpose(0, 1).contiguous()
-                recv = self.torch.empty_like(send)
-                self.dist.all_to_all_single(recv, send)
-            else:
-                recv = self.buf[:m].view(1, m, sl)
-            for j, k in enumerate(ks):
-                for src in range(N):            # pass src + N*k: ascending pass order
-                    if src + N * k < self.passes:
-                        self.slice.add_(recv[src, j])
+                    self.render_passes(mine, out[:len(mine)])
+            step = self.xrounds if self.async_render is not None else m
+            for s0 in range(0, m, step):
+                s1 = min(s0 + step, m)
+                mine_here = [j for j in range(s0, s1) if j < len(mine)]
+                if self.async_render is not None:
+                    for j in mine_here:         # passes in flight finish in any order: wait for each
+                        self.async_render.wait(j)
+                if mine_here and self.stage is not None:
+                    self.buf[mine_here[0]:mine_here[-1] + 1, :self.pixels3].copy_(
+                        self.stage[mine_here[0]:mine_here[-1] + 1])
+                n = s1 - s0
+                if N > 1:
+                    # send[d, j] = slice d of this rank's pass framebuffer of round ks[s0 + j]; every rank
+                    # issues the same sequence of exchanges (it depends only on m and the step)
+                    send = self.buf[s0:s1].view(n, N, sl).transpose(0, 1).contiguous()
+                    recv = self.torch.empty_like(send)
+                    self.dist.all_to_all_single(recv, send)
+                else:
+                    recv = self.buf[s0:s1].view(1, n, sl)
+                for j in range(n):
+                    for src in range(N):            # pass src + N*k: ascending pass order
+                        if src + N * ks[s0 + j] < self.passes:
+                            self.slice.add_(recv[src, j])
+            if mine and self.async_render is not None:
+                self.async_render.finish()
             done += len(mine)
         return done
 

@@ -176,6 +176,15 @@ int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer *
  * also stored there.  Blocking. */
 int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride,
                     float *d_pass_sums, rt_stats *stats);
+/* The same passes enqueued without waiting (d_pass_sums required, not for pixel tiles with sort
+ * on): rt_renderer_wait_pass makes a caller's HIP stream (a hipStream_t on r's device) wait until
+ * the k-th pass of the run (0-based) has written its sums, so the caller can exchange finished
+ * passes while later ones render (the multi-GPU slice exchange); rt_renderer_finish waits for the
+ * whole run and fills stats.  The framebuffer adds and every other rule are those of
+ * rt_renderer_run.  No reference counterpart (the reference's gpu_raytrace returned at the end). */
+int rt_renderer_run_async(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride, float *d_pass_sums);
+int rt_renderer_wait_pass(rt_renderer *r, int32_t k, void *hip_stream);
+int rt_renderer_finish(rt_renderer *r, rt_stats *stats);
 /* Same, with the per-pass sums returned in host memory (count*W*H*3 floats). */
 int rt_renderer_run_host(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride,
                          float *host_pass_sums, rt_stats *stats);

@@ -26,7 +26,29 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, out_path, chunk):
+class LazyAsyncRender:
+    """The asynchronous renderer's contract (rtamd.Renderer.run_async / wait_pass / finish) with the
+    oracle's pass sums, each rendered only when the frame waits for that pass (or at finish): a pass
+    the frame used before waiting for it would still be zeros, and the frame would not be exact."""
+
+    def __init__(self, sc):
+        self.sc, self.todo = sc, {}
+
+    def start(self, passes, out):
+        out.zero_()
+        self.todo = {j: (p, out[j]) for j, p in enumerate(passes)}
+
+    def wait(self, j):
+        p, row = self.todo.pop(j, (None, None))
+        if p is not None:
+            row.copy_(torch.from_numpy(self.sc.pass_sums(sort=True, pass_begin=p, pass_count=1, threads=2)[0]))
+
+    def finish(self):
+        for j in list(self.todo):
+            self.wait(j)
+
+
+def _worker(rank, world, port, out_path, chunk, xrounds=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sc = O.OracleScene(os.path.join(O.ASSETS, "cornell_plus.scene"), image=IMAGE)
@@ -35,7 +57,8 @@ def _worker(rank, world, port, out_path, chunk):
         for j, p in enumerate(passes):
             out[j].copy_(torch.from_numpy(sc.pass_sums(sort=True, pass_begin=p, pass_count=1, threads=2)[0]))
 
-    frame = D.PassShardedFrame(dist, torch, sc.pixels * 3, sc.passes, "cpu", render_passes, max_rounds_per_call=chunk)
+    frame = D.PassShardedFrame(dist, torch, sc.pixels * 3, sc.passes, "cpu", render_passes, max_rounds_per_call=chunk,
+                               async_render=LazyAsyncRender(sc) if xrounds else None, exchange_rounds=xrounds or 4)
     n = frame.run_all()
     assert n == len(D.pass_schedule(rank, world, sc.passes))
     if rank == 0:
@@ -43,10 +66,12 @@ def _worker(rank, world, port, out_path, chunk):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunk", [(2, 2), (3, None), (5, None)])
-def test_pass_sharded_frame_is_bitexact(tmp_path, world, chunk):
+@pytest.mark.parametrize("world,chunk,xrounds", [(2, 2, None), (3, None, None), (5, None, None),
+                                                 (2, None, 1), (3, 2, 1), (2, None, 2)])
+def test_pass_sharded_frame_is_bitexact(tmp_path, world, chunk, xrounds):
+    """xrounds: the overlapped exchange (an asynchronous renderer, slices exchanged every xrounds rounds)."""
     out = str(tmp_path / "fb.npy")
-    mp.spawn(_worker, args=(world, _free_port(), out, chunk), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, chunk, xrounds), nprocs=world, join=True)
     got = np.load(out)
     ref, _ = O.OracleScene(os.path.join(O.ASSETS, "cornell_plus.scene"), image=IMAGE).render(sort=True)
     assert np.array_equal(got, ref)

@@ -123,6 +123,17 @@ def main():
             # exclusive launch durations of the same profiled run (the profiler serialises dispatches),
             # in dispatch order per trace kernel variant: the denominator of the fabric-bytes rate
             durs = [round(d["dur_ms"], 5) for (k, _), d in disp.items() if k in trace and "dur_ms" in d]
+            # the same bytes launch by launch (bounce b = the b-th trace dispatch of the pass)
+            per = []
+            for (k, _), d in disp.items():
+                if k not in trace:
+                    continue
+                dd = derive(d)
+                rd1 = dd.get("read_bytes_by_size") or 2 * dd.get("fetch_size_bytes", 0)
+                wr1 = dd.get("write_bytes_by_size") or dd.get("write_size_bytes", 0)
+                per.append(int(rd1 + wr1))
+            if per and passes == 1:
+                rec["trace_bytes_by_launch"] = per
             if durs:
                 rec["trace_dur_ms_per_launch"] = durs
                 rec["trace_dur_ms_avg"] = sum(durs) / len(durs)
