@@ -284,45 +284,6 @@ __device__ __forceinline__ bool ray_triangle_flat(V3 o, V3 d, V3 p1, V3 e1, V3 e
     return ok_a & ok_u & ok_v & ok_t;
 }
 
-// The closest-independent part of ray_triangle_flat: the hit's t and whether a, u, v accept it.
-// The caller applies the t test (!(t < kEps || t >= closest)) later, against the closest of that
-// moment, so the outcome is ray_triangle_flat's bit for bit.
-__device__ __forceinline__ bool ray_triangle_uv(V3 o, V3 d, V3 p1, V3 e1, V3 e2, float &t) {
-    const V3 h = cross(d, e2);
-    const float a = dot(h, e1);
-    const float f = 1 / a;
-    const V3 s = o - p1;
-    const float u = dot(s, h) * f;
-    const V3 q = cross(s, e1);
-    const float v = dot(d, q) * f;
-    t = dot(e2, q) * f;
-    const bool ok_a = a != 0;
-    const bool ok_u = !(u < 0 || u > 1);
-    const bool ok_v = !(v < 0 || u + v > 1);
-    return ok_a & ok_u & ok_v;
-}
-
-// Wave-wide inclusive scans (DPP row shifts within rows of 16, then the gfx9 row broadcasts;
-// every lane must be active).
-__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
-    return v;
-}
-
 // Triangle range [ti, te) of a leaf ref (small leaves inline, big ones through big_leaves).
 __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int &ti, int &te) {
     if (ref & kBigLeaf) {
@@ -350,37 +311,14 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #ifndef RT_SORT_GRID
 #define RT_SORT_GRID 0                // cap on the reorder's hist/scatter grid (0: 8 blocks per CU)
 #endif
-// Parallel leaves (later bounces): a lane that reaches a leaf waits; once RT_LEAFPAR lanes of the
-// wave wait (or no lane has a node step left), their leaves' triangles are dealt to all 64 lanes,
-// one triangle test per lane, and each owner merges its leaf's results in triangle order.  0 = off
-// (one triangle per lane and step).
-#ifndef RT_LEAFPAR
-#define RT_LEAFPAR 0
-#endif
-// Later-bounce kernels may ask for fewer waves per SIMD as the minimum (RT_TRACE_WPE_LATER 7: the
-// allocator then still lands at <= 64 VGPRs, 8 waves, but without the SGPR spills to VGPR lanes it
-// makes under a hard 8); the bounce-0 kernels keep RT_TRACE_WPE.
-#ifndef RT_TRACE_WPE_LATER
-#define RT_TRACE_WPE_LATER RT_TRACE_WPE
-#endif
-#ifndef RT_LEAFPAR_WPE
-#define RT_LEAFPAR_WPE 7
-#endif
-template <bool SORTED, bool COUNT, int FIRST, bool LEAF = false>
-__global__ __launch_bounds__(kBlock)
-__attribute__((amdgpu_waves_per_eu((LEAF && FIRST == 0 && RT_LEAFPAR > 0) ? RT_LEAFPAR_WPE
-                                   : (FIRST == 0 ? RT_TRACE_WPE_LATER : RT_TRACE_WPE),
-                                   RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8))) void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8)))
+template <bool SORTED, bool COUNT, int FIRST>
+__global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
                                                        unsigned long long *__restrict__ tspan) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
-    constexpr bool kLeafPar = RT_LEAFPAR > 0 && FIRST == 0 && LEAF;
-    // parallel leaves: 64 words per wave, written and read by different lanes of the wave (relaxed
-    // wavefront-scope atomics around a fence: plain ds ops, which the compiler neither forwards from a
-    // lane's own store nor reorders; one wave's LDS operations complete in order)
-    __shared__ uint32_t owner_tab[kLeafPar ? kBlock : 1];
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
     // before its first wave and the stream's marker packets (what rocprofv3 reports).  The start is
@@ -616,85 +554,6 @@ __attribute__((amdgpu_waves_per_eu((LEAF && FIRST == 0 && RT_LEAFPAR > 0) ? RT_L
             if (mixed) PROF(9, min(__popcll(lf), __popcll(act & ~lf)));
         }
 #endif
-        if constexpr (kLeafPar) {
-            // One memory round trip per iteration for both kinds of work: the node lanes' records and
-            // (when the leaf phase runs) the dealt triangles are in flight together.
-            const uint32_t lane = lane_id();
-            const bool node_lane = slot >= 0 && !(ti < te);
-            const unsigned long long waiting = __ballot(slot >= 0 && ti < te);
-            const bool do_leaf = __popcll(waiting) >= RT_LEAFPAR || (waiting && !__ballot(node_lane));
-            float4 a{0, 0, 0, 0}, b{0, 0, 0, 0}, c{0, 0, 0, 0};
-            uint2 kids{0, 0};
-            if (node_lane) {
-                const float4 *rec = S.nodes + (size_t)ref * 4;
-                a = rec[0]; b = rec[1]; c = rec[2];
-                kids = *reinterpret_cast<const uint2 *>(rec + 3);
-            }
-            // ---- waiting leaves: their triangles dealt over the wave's lanes in lane order (position
-            // p = one triangle), loaded now; tested after the node step, then merged by each owner in
-            // triangle order (the reference's sequence of closest updates)
-            uint32_t cnt = 0, start = 0;
-            int src = (int)lane;
-            bool worker = false;
-            float4 q0{0, 0, 0, 0}, q1{0, 0, 0, 0};
-            float q2 = 0;
-            if (do_leaf) {
-                cnt = (slot >= 0 && ti < te) ? (uint32_t)min(te - ti, 64) : 0u;
-                const uint32_t incl = wave_incl_add(cnt);
-                const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                start = incl - cnt;
-                uint32_t *tab = owner_tab + (threadIdx.x & ~63u);
-                __hip_atomic_store(tab + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                if (cnt && start < 64)
-                    __hip_atomic_store(tab + start, lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                const uint32_t own = wave_incl_max(   // owner lane + 1 of triangle position `lane`
-                    __hip_atomic_load(tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
-                worker = lane < total;
-                src = worker ? (int)own - 1 : (int)lane;
-                const int base = __shfl(ti - (int)start, src);   // triangle of position p = base + p
-                if (worker) {
-                    const float4 *rec = S.tris + (size_t)(base + (int)lane) * 3;
-                    q0 = rec[0]; q1 = rec[1]; q2 = rec[2].x;
-                }
-            }
-            // ---- node lanes: one internal node each (a lane standing on a leaf waits)
-            if (__ballot(node_lane)) {
-                bool need = false;
-                if (node_lane) need = node_step(a, b, c, kids);
-                pop_loop(need);
-            }
-            if (do_leaf) {
-                // the owners' rays (unchanged by the node step: an owner was not a node lane)
-                const V3 wo = v3(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
-                const V3 wd = v3(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
-                // t where a, u and v accept the hit, else -1 (which the t test rejects as the
-                // reference's early-outs do); a NaN t stays NaN and is accepted as in the reference
-                float tv = -1.0f;
-                if (worker) {
-                    float t;
-                    tv = ray_triangle_uv(wo, wd, v3(q0.x, q0.y, q0.z), v3(q0.w, q1.x, q1.y), v3(q1.z, q1.w, q2), t)
-                             ? t : -1.0f;
-                }
-                const uint32_t ce = (cnt && start < 64) ? min(cnt, 64u - start) : 0u;   // this round's share
-                for (uint32_t k0 = 0; __ballot(k0 < ce); k0 += 4) {   // four positions' results per exchange
-                    float tk[4];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) tk[j] = __shfl(tv, k0 + j < ce ? (int)(start + k0 + j) : (int)lane);
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const bool take = k0 + j < ce && !(tk[j] < kEps || tk[j] >= closest);
-                        closest = take ? tk[j] : closest;
-                        index = take ? S.sphere_count + ti + (int)(k0 + j) : index;
-                    }
-                }
-                if (COUNT) tt += ce;
-                ti += (int)ce;
-                pop_loop(ce && ti == te);
-            }
-            continue;
-        }
         if (slot < 0) continue;
         // ---- one step: a single triangle test of the current leaf, or one internal node
         // (both children's slabs).  One triangle per step keeps the leaf branch as short as the
@@ -1515,8 +1374,6 @@ struct rt_renderer {
     DevBuf<Counters> ctr;
     DevBuf<unsigned long long> tspans;   // per run: [pass][bounce] trace-launch wall-clock spans (event timing on)
     int wall_khz = 0;                    // device wall clock rate (wall_clock64 ticks per ms)
-    // parallel-leaf trace (RT_LEAFPAR builds) from this bounce on (RTAMD_LEAFPAR_FROM, default 1)
-    int leafpar_from = std::getenv("RTAMD_LEAFPAR_FROM") ? std::atoi(std::getenv("RTAMD_LEAFPAR_FROM")) : 1;
     // rt_renderer_launch_profile: the last event-timed run's first pass, per bounce
     std::vector<double> launch_ms;
     std::vector<uint32_t> launch_live;
@@ -1826,11 +1683,7 @@ struct rt_renderer {
             uint32_t *hist = shade_hist && !last ? c.sort_counts.p : nullptr;   // the shade kernel counts the buckets
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
-        if (!inline_hits && RT_LEAFPAR > 0 && FIRST == 0 && b >= leafpar_from)                                   \
-            hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST, true>), dim3(tgrid), dim3(kBlock), 0, st, ds, \
-                               pa, c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p,                          \
-                               tspan ? tspan + kSpanWords * b : nullptr);                                        \
-        else if (!inline_hits)                                                                                   \
+        if (!inline_hits)                                                                                        \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
                                c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr); \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \

@@ -43,9 +43,28 @@ def rccl():
     dist.destroy_process_group()
 
 
+class AsyncPasses:
+    """bench.py's asynchronous renderer adapter: rt_renderer_run_async / wait_pass / finish."""
+
+    def __init__(self, ren, torch):
+        self.ren, self.torch = ren, torch
+
+    def start(self, passes, out):
+        stride = passes[1] - passes[0] if len(passes) > 1 else 1
+        self.ren.run_async(passes[0], len(passes), stride, out.data_ptr())
+
+    def wait(self, j):
+        self.ren.wait_pass(j, self.torch.cuda.current_stream().cuda_stream)
+
+    def finish(self):
+        self.ren.finish()
+
+
 @pytest.mark.parametrize("sort", [True, False])
-@pytest.mark.parametrize("chunk", [1, 2, None])
-def test_pass_sharded_frame_rccl_world1(rccl, sort, chunk):
+@pytest.mark.parametrize("chunk,xrounds", [(1, None), (2, None), (None, None), (None, 1), (None, 2), (2, 1)])
+def test_pass_sharded_frame_rccl_world1(rccl, sort, chunk, xrounds):
+    """xrounds: the overlapped exchange (rt_renderer_run_async; torch's stream waits on per-pass events
+    and adds the slices of every xrounds rounds while later passes render)."""
     torch, dist = rccl
     path = "%s/cornell_plus.scene" % R.ASSETS
     ref, _ = O.OracleScene(path, image=IMAGE).render(sort=sort)
@@ -57,7 +76,8 @@ def test_pass_sharded_frame_rccl_world1(rccl, sort, chunk):
             ren.run(pass_begin=passes[0], count=len(passes), stride=stride, d_pass_sums=out.data_ptr())
 
         frame = D.PassShardedFrame(dist, torch, psc.pixels * 3, psc.passes, torch.device("cuda", 0), render_passes,
-                                   max_rounds_per_call=chunk)
+                                   max_rounds_per_call=chunk, async_render=AsyncPasses(ren, torch) if xrounds else None,
+                                   exchange_rounds=xrounds or 4)
         for attempt in range(2):            # the second frame reuses every buffer of the first
             frame.reset()
             assert frame.run_all() == psc.passes

@@ -2,13 +2,13 @@
 BASELINE config x GPUs.  1-GPU cells come from profiles/<round>/bench_*.json and profiles/pmc_traffic.json;
 N > 1 has no hardware measurement (the driver's SCALE run is the only one), so those rows say so.
 
-    python tools/results_table.py [profiles/r03]"""
+    python tools/results_table.py [profiles/r04/final]"""
 import json
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-D = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r03")
+D = os.path.abspath(sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r04", "final"))
 ROWS = [("1 cornell 256² × 64 × 4", "bench_cornell.json"),
         ("2 cornell_plus 512² × 256 × 8", "bench_cornell_plus.json"),
         ("3 spheres 1024² × 1024 × 8", "bench_spheres.json"),
@@ -51,10 +51,10 @@ def main():
         occ = "8 waves/SIMD (64 VGPRs)" if r else "— (no trace kernel)" if "spheres" in name else "8 waves/SIMD"
         cpu = "%.1f (%d, %s)" % (cb["frame_s"], cb["cores"], "extrapolated" if cb.get("extrapolated") else "full frame") \
             if cb.get("frame_s") is not None else "—"
-        print("| %s | 1 | %s | %s | %.0f | %.0f | %s | %s | %s | %s | %s | profiles/r03/final/%s |" % (
+        print("| %s | 1 | %s | %s | %.0f | %.0f | %s | %s | %s | %s | %s | %s |" % (
             name, d.get("render_wall_ms"), "%.1f" % km if km else "—", d["value"], d["config"]["nominal_mrays_per_s"],
             "%.0f (%.3f)" % (fr["achieved"], fr["frac"]) if fr else "—", "%.3f" % va["frac"] if va else "—", occ,
-            d.get("bit_exact_vs_oracle"), cpu, f))
+            d.get("bit_exact_vs_oracle"), cpu, os.path.relpath(os.path.join(D, f), REPO)))
         print("| %s | 2 / 4 / 8 | unmeasured on hardware (no multi-GPU node here; the driver's SCALE run) "
               "| | | | | | | | | |" % name)
 
