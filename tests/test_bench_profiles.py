@@ -1,6 +1,6 @@
 """The committed PMC summaries that bench.py prices its roofline with (profiles/pmc_traffic.json,
 profiles/pmc_issue.json) are present for the headline workload, come from exactly one profiled pass,
-and give fractions <= 1 at the measured pass time (profiles/r02/bench_teapot.json)."""
+and give fractions <= 1 at the measured pass time (profiles/r04/final/bench_teapot.json)."""
 import importlib
 import json
 import os
@@ -19,7 +19,7 @@ def _bench():
 
 
 def _bench_line():
-    with open(os.path.join(REPO, "profiles", "r02", "bench_teapot.json")) as f:
+    with open(os.path.join(REPO, "profiles", "r04", "final", "bench_teapot.json")) as f:
         return json.loads(f.read().strip().splitlines()[-1])
 
 
@@ -70,7 +70,7 @@ def test_roofline_restated_on_exclusive_launches():
 
 
 def _final_lines():
-    d = os.path.join(REPO, "profiles", "r03", "final")
+    d = os.path.join(REPO, "profiles", "r04", "final")
     out = {}
     for f in sorted(os.listdir(d)):
         if f.startswith("bench_") and f.endswith(".json"):
@@ -80,7 +80,7 @@ def _final_lines():
 
 
 def test_closing_lines_every_config_bit_exact():
-    """Round 3's closing measurement (profiles/r03/final): a line per BASELINE config, each with its pass-0
+    """Round 4's closing measurement (profiles/r04/final): a line per BASELINE config, each with its pass-0
     framebuffer hash equal to the oracle's and its fractions at most one."""
     lines = _final_lines()
     for name in ("bench_cornell.json", "bench_cornell_plus.json", "bench_spheres.json", "bench_teapot.json",
@@ -109,7 +109,24 @@ def test_closing_exclusive_launch_agrees_with_the_profiler():
 def test_results_table_from_committed_files():
     import subprocess
     out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "results_table.py"),
-                          os.path.join(REPO, "profiles", "r03", "final")], capture_output=True, text=True, check=True).stdout
+                          os.path.join(REPO, "profiles", "r04", "final")], capture_output=True, text=True, check=True).stdout
     rows = [r for r in out.splitlines() if r.startswith("| ") and " | 1 | " in r]
     assert len(rows) == 7, out                      # 5 configs, teapot and lamp in both sort modes
     assert all("| True |" in r for r in rows)
+
+
+def test_roofline_per_launch_table_recomputes():
+    """Round 4: the per-launch table (rt_renderer_launch_profile) of the closing line: every launch's fraction
+    follows from its own bytes and duration, heavy + tail cover the launches, and the measured bytes come from the
+    committed PMC record of the same revision."""
+    bench = _bench()
+    roof = _bench_line()["roofline"]
+    rows = roof["per_launch"]
+    assert len(rows) == 16 and [r["bounce"] for r in rows] == list(range(16))
+    for r in rows:
+        assert abs(r["frac"] - r["algorithmic_bytes"] / (r["ms"] / 1e3) / 1e9 / bench.HBM_PEAK_GBS) < 2e-4
+    assert roof["heavy"]["launches"] + roof["tail"]["launches"] == 16
+    assert roof["heavy"]["live"] + roof["tail"]["live"] == sum(r["live"] for r in rows)
+    pmc = bench.load_pmc(WORKLOAD)
+    assert [r["measured_bytes"] for r in rows] == pmc["trace_bytes_by_launch"]
+    assert pmc["run"].startswith("rev ")
