@@ -311,6 +311,9 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #ifndef RT_SORT_GRID
 #define RT_SORT_GRID 0                // cap on the reorder's hist/scatter grid (0: 8 blocks per CU)
 #endif
+#ifndef RT_DIAG
+#define RT_DIAG 0                     // diagnostic timing builds (wrong images): 1 no acc store, 2 no env, 3 no normal
+#endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8)))
 template <bool SORTED, bool COUNT, int FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
@@ -566,8 +569,14 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         bool need = false;              // the lane needs the next node from its stack
         const bool in_leaf = ti < te;
         const float4 *rec = in_leaf ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4;
+        // The child refs are loaded by node lanes only: a leaf lane's step is 3 L1 accesses instead
+        // of 4, and the gather rate of L1 accesses bounds the heavy bounces (tools/experiments/
+        // gather_bench.hip).  Round 4, A/B on one box: teapot 20 steps 6.89 -> 6.81, full frame
+        // 6.71 -> 6.61, lamp 12.94 -> 12.70 ms/pass (profiles/r04/ab_kids.txt).  Loading only e2.z
+        // for leaf lanes as well (a divergent one-dword load) was slower: 7.74.
         const float4 a = rec[0], b = rec[1], c = rec[2];
-        const uint2 kids = *reinterpret_cast<const uint2 *>(rec + 3);   // node lanes only use it
+        uint2 kids = make_uint2(0, 0);
+        if (!in_leaf) kids = *reinterpret_cast<const uint2 *>(rec + 3);
         if (in_leaf) {
             const float4 q0 = a, q1 = b;
             const float q2 = c.x;
@@ -674,7 +683,11 @@ __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &p
     }
     V3 no = o, nd = d;
     if (index == -1) {
+#if RT_DIAG == 2
+        C = C + d * T;                  // diagnostic timing build only: no environment lookup
+#else
         C = C + sky_color(S.env, S.env_w, S.env_h, d) * T;
+#endif
         T = v3(0, 0, 0);
     } else {
         no = o + closest * d;
@@ -683,8 +696,12 @@ __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &p
             const float4 sph = S.spheres[index];
             normal = (1 / sph.w) * (no - v3(sph.x, sph.y, sph.z));
         } else {
+#if RT_DIAG == 3
+            normal = v3(0.f, 1.f, 0.f);     // diagnostic timing build only: no triangle normal load
+#else
             const float4 q2 = S.tris[(size_t)(index - S.sphere_count) * 3 + 2];
             normal = v3(q2.y, q2.z, q2.w);
+#endif
         }
         scatter(d, normal, load_mat(S.mats + (size_t)S.mat_idx[index] * 3), rng, T, C, nd);
     }
@@ -726,7 +743,7 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
             geo[(size_t)slot * 2] = make_float4(no.x, no.y, no.z, nd.x);
             geo[(size_t)slot * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
         }
-        if (dead || last) acc[sh.ray] = tcv;
+        if ((dead || last) && RT_DIAG != 1) acc[sh.ray] = tcv;   // RT_DIAG 1: timing build without it
         else if (!FUSED) tc[slot] = tcv;   // FUSED: the reorder replays the shading instead
         const uint32_t bk = dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u);
         if (!last) bkt[slot] = (uint8_t)bk;
