@@ -52,27 +52,6 @@ namespace {
 #ifndef RT_CHUNK_MAX
 #define RT_CHUNK_MAX 128
 #endif
-#ifndef RT_SHADE_PREFETCH
-#define RT_SHADE_PREFETCH 0
-#endif
-#ifndef RT_SCATTER_PREFETCH
-#define RT_SCATTER_PREFETCH 0
-#endif
-#ifndef RT_PCG_OPAQUE
-#define RT_PCG_OPAQUE 1
-#endif
-#ifndef RT_ACC_NT
-#define RT_ACC_NT 1
-#endif
-#ifndef RT_STREAM_ST
-#define RT_STREAM_ST 0
-#endif
-#ifndef RT_STREAM_LD
-#define RT_STREAM_LD 0
-#endif
-#ifndef RT_DIAG
-#define RT_DIAG 0                     // diagnostic timing builds (wrong images): 1 no acc store, 2 no env lookup
-#endif
 #ifndef RT_INFLIGHT
 #define RT_INFLIGHT 20                // with 24 HW queues: +1.5 % teapot, +3.4 % lamp over 16 (24 in flight: worse)
 #endif
@@ -244,14 +223,12 @@ struct PassArgs {
 
 __device__ __forceinline__ V3 primary_dir(const DevScene &S, int i, const PassArgs &pa) {
     Rng rng = pcg_seed((uint32_t)i * 0x85810BEAu + pa.gen_seed_term);   // 298592570346 mod 2^32
-#if RT_PCG_OPAQUE
     // the increment made opaque where it is used: as a loop-invariant 64-bit constant the compiler
     // hoisted it (and its `| 1`) out of the trace kernel's loop and spilled both to scratch, so
     // every bounce-0 refill waited for two scratch reloads
     uint32_t z;
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));
     rng.inc += z;
-#endif
     const uint32_t pixel = pa.by_rtc.div((uint32_t)i);
     const uint32_t yy = pa.by_width.div(pixel);
     const int x = (int)(pixel - yy * (uint32_t)S.width), y = (int)yy;
@@ -259,38 +236,6 @@ __device__ __forceinline__ V3 primary_dir(const DevScene &S, int i, const PassAr
     const float yc = (y + random01(rng)) * S.inv_h;
     return normalise(S.tl + xc * S.sr - yc * S.su);
 }
-
-// Streaming accesses (RT_STREAM_ST / RT_STREAM_LD): ray state, hits, buckets and radiance are far
-// larger than the caches and each is read once by the next kernel, so their stores (and loads) carry
-// the nontemporal hint and leave the L2 to the scene records the trace kernels re-read.
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef float f2v __attribute__((ext_vector_type(2)));
-template <bool NT> __device__ __forceinline__ void st_s(float4 *p, float4 v) {
-    if (NT) __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v *>(p));
-    else *p = v;
-}
-template <bool NT> __device__ __forceinline__ void st_s(float2 *p, float2 v) {
-    if (NT) __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v *>(p));
-    else *p = v;
-}
-template <bool NT, typename U> __device__ __forceinline__ void st_s(U *p, U v) {
-    if (NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-template <bool NT> __device__ __forceinline__ float4 ld_s(const float4 *p) {
-    if (!NT) return *p;
-    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-template <bool NT> __device__ __forceinline__ float2 ld_s(const float2 *p) {
-    if (!NT) return *p;
-    const f2v v = __builtin_nontemporal_load(reinterpret_cast<const f2v *>(p));
-    return make_float2(v.x, v.y);
-}
-template <bool NT, typename U> __device__ __forceinline__ U ld_s(const U *p) {
-    return NT ? __builtin_nontemporal_load(p) : *p;
-}
-constexpr bool kStSt = RT_STREAM_ST != 0, kStLd = RT_STREAM_LD != 0;
 
 // ---------------------------------------------------------------- traversal
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -528,7 +473,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             // step's vmcnt(0) waits (before its record loads, before an LDS pop) wait for the write as
             // well; here the stores overlap the refill's own ray loads (A/B 7.13 -> 7.00 ms/pass)
             if (slot <= -2) {
-                st_s<kStSt>(hits + (-2 - slot), make_float2(closest, __int_as_float(index)));
+                hits[-2 - slot] = make_float2(closest, __int_as_float(index));
                 slot = -1;
             }
             bool fresh = false;
@@ -563,8 +508,8 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                         d = primary_dir(S, (int)first_ray<FIRST>(pa.map, (uint32_t)slot), pa);
                     } else {
                         const float4 *rp = geo + (size_t)slot * 2;   // ray state is in slot order
-                        const float4 r0 = ld_s<kStLd>(rp);
-                        const float2 r1 = ld_s<kStLd>(reinterpret_cast<const float2 *>(rp + 1));
+                        const float4 r0 = rp[0];
+                        const float2 r1 = *reinterpret_cast<const float2 *>(rp + 1);
                         o = v3(r0.x, r0.y, r0.z);
                         d = v3(r0.w, r1.x, r1.y);
                     }
@@ -585,7 +530,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
                     if (ref & kLeaf) {
                         leaf_range(S, ref, ti, te);
                         if (ti == te) {  // no triangles at all: spheres only
-                            st_s<kStSt>(hits + slot, make_float2(closest, __int_as_float(index)));
+                            hits[slot] = make_float2(closest, __int_as_float(index));
                             slot = -1;
                         }
                     }
@@ -653,7 +598,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 #endif
         pop_loop(need);
     }
-    if (slot <= -2) st_s<kStSt>(hits + (-2 - slot), make_float2(closest, __int_as_float(index)));
+    if (slot <= -2) hits[-2 - slot] = make_float2(closest, __int_as_float(index));
     Counters *cs = ctr + ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kCtrSlots - 1));
     const unsigned long long nl = wave_sum(nlive);
     if (COUNT) {
@@ -691,8 +636,9 @@ struct Shaded {
 };
 // INLINE (scenes without triangles): the closest hit is the sphere loop (scene.cu:338-372),
 // computed here instead of read from the trace kernel's output.
-// A slot's coalesced inputs (hit record, ray id, seed slot, state), loaded apart from the shading so
-// that the shade kernel can issue the next round's loads before shading this one (RT_SHADE_PREFETCH).
+// A slot's coalesced inputs (hit record, ray id, seed slot, state), loaded apart from the shading.
+// (Round 4 measured issuing the next round's inputs before shading this one, in the shade and the
+// fused scatter-shade kernels: 72-90 VGPRs, no gain.)
 struct ShadeIn {
     float2 h;
     uint32_t ray, seed;
@@ -708,15 +654,15 @@ __device__ __forceinline__ ShadeIn shade_in(const PassArgs &pa, int slot, const 
     // reference slot is the ray id (pixel-tile renders: mapped from this tile's slot).
     const uint32_t ray0 = first_ray<FIRST>(pa.map, (uint32_t)slot);   // bounce 0 only
     // Pixel tiles with the reorder on: the global post-sort slot, carried per ray (seed_of).
-    in.seed = (!FIRST && seed_of) ? seed_of[slot] : (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : ld_s<kStLd>(rid + slot);
-    if (!INLINE) in.h = ld_s<kStLd>(hits + slot);
+    in.seed = (!FIRST && seed_of) ? seed_of[slot] : (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
+    if (!INLINE) in.h = hits[slot];
     // the ray id goes out with the state loads (issued at its use, it was a round trip of its own
     // between the shading and the stores)
-    in.ray = FIRST ? (FIRST == 2 ? ray0 : (uint32_t)slot) : ld_s<kStLd>(rid + slot);
+    in.ray = FIRST ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
     if (!FIRST) {
-        in.r0 = ld_s<kStLd>(geo + (size_t)slot * 2);
-        in.r1 = ld_s<kStLd>(geo + (size_t)slot * 2 + 1);
-        in.r2 = ld_s<kStLd>(tc + slot);
+        in.r0 = geo[(size_t)slot * 2];
+        in.r1 = geo[(size_t)slot * 2 + 1];
+        in.r2 = tc[slot];
     }
     return in;
 }
@@ -756,11 +702,7 @@ __device__ __forceinline__ Shaded shade_from(const DevScene &S, const PassArgs &
     }
     V3 no = o, nd = d;
     if (index == -1) {
-#if RT_DIAG == 2
-        C = C + d * T;                  // diagnostic timing build only: no environment lookup
-#else
         C = C + sky_color(S.env, S.env_w, S.env_h, d) * T;
-#endif
         T = v3(0, 0, 0);
     } else {
         // The material index and the surface record (sphere, or the triangle quad holding the
@@ -815,8 +757,8 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
     const int L = (int)__builtin_amdgcn_readfirstlane(*live_count);
     unsigned hit = 0, miss = 0, hit_sphere = 0;
     // one slot's shading and new state; returns its bucket
-    auto shade_slot_in = [&](int slot, const ShadeIn &in) -> uint32_t {
-        const Shaded sh = shade_from<SORTED, FIRST, INLINE>(S, pa, slot, in, seed_term);
+    auto shade_slot = [&](int slot) -> uint32_t {
+        const Shaded sh = shade_one<SORTED, FIRST, INLINE>(S, pa, slot, geo, tc, rid, hits, seed_term, seed_of);
         const V3 no = sh.no, nd = sh.nd, T = sh.T, C = sh.C;
         miss += sh.kind == 0;
         hit += sh.kind != 0;
@@ -824,25 +766,21 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
         const bool dead = is_black(T);
         const float4 tcv = make_float4(T.z, C.x, C.y, C.z);
         if (!FUSED && !dead && !last) {     // a terminated ray's geometry is never read again
-            st_s<kStSt>(geo + (size_t)slot * 2, make_float4(no.x, no.y, no.z, nd.x));
-            st_s<kStSt>(geo + (size_t)slot * 2 + 1, make_float4(nd.y, nd.z, T.x, T.y));
+            geo[(size_t)slot * 2] = make_float4(no.x, no.y, no.z, nd.x);
+            geo[(size_t)slot * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
         }
-        if ((dead || last) && RT_DIAG != 1) {   // RT_DIAG 1: timing build without it
-#if RT_ACC_NT
+        if (dead || last) {
+            // scattered 16-B writes (rays terminate in sorted, not ray-id, order): nontemporal, so
+            // the radiance lines do not displace the scene records the trace kernels re-read from
+            // L2 (round 4: later-bounce shade 1.73 -> 1.45 ms alone, teapot 20 steps 6.73 -> 6.41
+            // ms/pass; the same hint on the coalesced ray-state, hit and bucket traffic: +1-2 %)
             typedef float f4v __attribute__((ext_vector_type(4)));
-            const f4v v = {tcv.x, tcv.y, tcv.z, tcv.w};
-            __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(acc + sh.ray));   // scattered 16-B writes: stream past L2
-#else
-            acc[sh.ray] = tcv;
-#endif
+            __builtin_nontemporal_store(f4v{tcv.x, tcv.y, tcv.z, tcv.w}, reinterpret_cast<f4v *>(acc + sh.ray));
         }
-        else if (!FUSED) st_s<kStSt>(tc + slot, tcv);   // FUSED: the reorder replays the shading instead
+        else if (!FUSED) tc[slot] = tcv;   // FUSED: the reorder replays the shading instead
         const uint32_t bk = dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u);
-        if (!last) st_s<kStSt>(bkt + slot, (uint8_t)bk);
+        if (!last) bkt[slot] = (uint8_t)bk;
         return bk;
-    };
-    auto shade_slot = [&](int slot) -> uint32_t {
-        return shade_slot_in(slot, shade_in<SORTED, FIRST, INLINE>(pa, slot, geo, tc, rid, hits, seed_of));
     };
     if (counts && !last) {
         __shared__ uint32_t h[kBuckets];
@@ -852,24 +790,10 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
             __syncthreads();
             const int base = tile * span;
             const int rounds = min(R, (L - base + kBlock - 1) / kBlock);   // block-uniform: the last tile is short
-#if RT_SHADE_PREFETCH
-            // the next round's inputs are loaded before this round is shaded: they travel with this
-            // round's dependent loads instead of costing a round trip of their own
-            ShadeIn nxt{};
-            if (base + (int)threadIdx.x < L) nxt = shade_in<SORTED, FIRST, INLINE>(pa, base + threadIdx.x, geo, tc, rid, hits, seed_of);
-#endif
             for (int r = 0; r < rounds; r++) {
                 const int slot = base + r * kBlock + threadIdx.x;
                 const bool valid = slot < L;
-#if RT_SHADE_PREFETCH
-                const ShadeIn cur = nxt;
-                if (r + 1 < rounds && slot + kBlock < L)
-                    nxt = shade_in<SORTED, FIRST, INLINE>(pa, slot + kBlock, geo, tc, rid, hits, seed_of);
-                asm volatile("" ::: "memory");
-                const uint32_t bk = valid ? shade_slot_in(slot, cur) : 0u;
-#else
                 const uint32_t bk = valid ? shade_slot(slot) : 0u;
-#endif
                 const unsigned long long peers = match_bucket(bk, valid);
                 if (valid && rank_below(peers) == 0) atomicAdd(&h[bk], (uint32_t)__popcll(peers));
             }
@@ -1060,10 +984,10 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
         float4 g0 = make_float4(0, 0, 0, 0), g1 = g0, t = g0;
         uint32_t id = 0;
         if (move) {                     // issued before the ranking so the loads overlap it
-            g0 = ld_s<kStLd>(geo_in + (size_t)item * 2);
-            g1 = ld_s<kStLd>(geo_in + (size_t)item * 2 + 1);
-            t = ld_s<kStLd>(tc_in + item);
-            id = FIRST_SRC ? first_ray<FIRST_SRC>(map, (uint32_t)item) : ld_s<kStLd>(rid_in + item);
+            g0 = geo_in[(size_t)item * 2];
+            g1 = geo_in[(size_t)item * 2 + 1];
+            t = tc_in[item];
+            id = FIRST_SRC ? first_ray<FIRST_SRC>(map, (uint32_t)item) : rid_in[item];
         }
         uint32_t gs = 0;
         if (gslot_out && move) gs = newpos[FIRST_SRC ? first_ray<FIRST_SRC>(map, (uint32_t)item) : gslot_in[item]];
@@ -1074,10 +998,10 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
         if (move) {
             uint32_t pos = run[b] + rank;
             for (int k = 0; k < wave; k++) pos += wcount[k][b];
-            st_s<kStSt>(geo_out + (size_t)pos * 2, g0);
-            st_s<kStSt>(geo_out + (size_t)pos * 2 + 1, g1);
-            st_s<kStSt>(tc_out + pos, t);
-            st_s<kStSt>(rid_out + pos, id);
+            geo_out[(size_t)pos * 2] = g0;
+            geo_out[(size_t)pos * 2 + 1] = g1;
+            tc_out[pos] = t;
+            rid_out[pos] = id;
             if (gslot_out) gslot_out[pos] = gs;
         }
         __syncthreads();
@@ -1243,35 +1167,13 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
         const int wave = threadIdx.x >> 6;
         const int base = tile * span;
         const int rounds = min(R, (n - base + kBlock - 1) / kBlock);   // block-uniform: skips a short tile's empty rounds
-#if RT_SCATTER_PREFETCH
-        // the next round's bucket and inputs are loaded before this round is shaded
-        uint32_t b_nxt = 0;
-        ShadeIn in_nxt{};
-        if (base + (int)threadIdx.x < n) {
-            b_nxt = bkt_in[base + threadIdx.x];
-            in_nxt = shade_in<SORTED, FIRST, INLINE>(pa, base + threadIdx.x, geo_in, tc_in, rid_in, hits, nullptr);
-        }
-#endif
         for (int r = 0; r < rounds; r++) {
             const int item = base + r * kBlock + threadIdx.x;
             const bool valid = item < n;
-#if RT_SCATTER_PREFETCH
-            const uint32_t b = valid ? b_nxt : 0u;
-            const ShadeIn in_cur = in_nxt;
-            if (r + 1 < rounds && item + kBlock < n) {
-                b_nxt = bkt_in[item + kBlock];
-                in_nxt = shade_in<SORTED, FIRST, INLINE>(pa, item + kBlock, geo_in, tc_in, rid_in, hits, nullptr);
-            }
-            asm volatile("" ::: "memory");
-            const bool move = valid && b != kDead;
-            Shaded sh{};
-            if (move) sh = shade_from<SORTED, FIRST, INLINE>(S, pa, item, in_cur, seed_term);
-#else
             const uint32_t b = valid ? bkt_in[item] : 0u;
             const bool move = valid && b != kDead;
             Shaded sh{};
             if (move) sh = shade_one<SORTED, FIRST, INLINE>(S, pa, item, geo_in, tc_in, rid_in, hits, seed_term);
-#endif
             const unsigned long long peers = match_bucket(b, valid);
             const uint32_t rank = rank_below(peers);
             if (valid && rank == 0) wcount[wave][b] = (uint32_t)__popcll(peers);
@@ -1279,10 +1181,10 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
             if (move) {
                 uint32_t pos = run[b] + rank;
                 for (int k = 0; k < wave; k++) pos += wcount[k][b];
-                st_s<kStSt>(geo_out + (size_t)pos * 2, make_float4(sh.no.x, sh.no.y, sh.no.z, sh.nd.x));
-                st_s<kStSt>(geo_out + (size_t)pos * 2 + 1, make_float4(sh.nd.y, sh.nd.z, sh.T.x, sh.T.y));
-                st_s<kStSt>(tc_out + pos, make_float4(sh.T.z, sh.C.x, sh.C.y, sh.C.z));
-                st_s<kStSt>(rid_out + pos, sh.ray);
+                geo_out[(size_t)pos * 2] = make_float4(sh.no.x, sh.no.y, sh.no.z, sh.nd.x);
+                geo_out[(size_t)pos * 2 + 1] = make_float4(sh.nd.y, sh.nd.z, sh.T.x, sh.T.y);
+                tc_out[pos] = make_float4(sh.T.z, sh.C.x, sh.C.y, sh.C.z);
+                rid_out[pos] = sh.ray;
             }
             __syncthreads();
             if (threadIdx.x < kBuckets) {
@@ -1312,7 +1214,7 @@ __global__ __launch_bounds__(kBlock) void accumulate_kernel(const float4 *__rest
     const int n = np * rtc;
     const float4 *src = tc + (size_t)p0 * rtc;
     for (int e = threadIdx.x; e < n; e += kBlock) {
-        const float4 c = ld_s<kStLd>(TILED ? tc + (size_t)pix.ray((uint32_t)(p0 + e / rtc)) * rtc + e % rtc : src + e);
+        const float4 c = TILED ? tc[(size_t)pix.ray((uint32_t)(p0 + e / rtc)) * rtc + e % rtc] : src[e];
         col[e * 3] = c.y;
         col[e * 3 + 1] = c.z;
         col[e * 3 + 2] = c.w;
