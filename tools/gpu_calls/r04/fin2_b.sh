@@ -1,0 +1,3 @@
+# Round 4 second closing measurement, part B: PMC records and bench lines of the other BASELINE configs,
+# scaling probe, Table 1
+bash tools/pmc_configs.sh r4fin2 && bash tools/round_measure.sh r4fin2 B
