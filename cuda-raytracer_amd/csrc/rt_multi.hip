@@ -28,6 +28,7 @@
 // after every bounce but the last (nccl_exchange), and the frame is an ncclReduce of the owners'
 // framebuffers.
 #include "rt_abi.h"
+#include "mgpu_protocol.h"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -75,72 +76,15 @@ struct DevState {
     double exchange_ms = 0;
 };
 
-// A device that fails must not leave its peers blocked in a collective.  Every device first builds
-// its renderer and buffers (where nearly every failure happens: out of memory, a bad scene) and
-// meets the others; if any failed, all return before the first collective.  A failure after that
-// sets `failed`; every device aborts only its OWN communicator (its thread is the only one that
-// uses it, so no call can race the abort), when it fails itself or when it sees the flag: before
-// each RCCL call and while it polls a stream or event that waits on a collective.  The aborted
-// communicator's pending kernels end, and its peers' polls see the flag and abort theirs.
-struct Sync {
-    std::mutex m;
-    std::condition_variable cv;
-    int world = 0, arrived = 0;
-    bool setup_failed = false;
-    std::atomic<bool> failed{false};
-    bool setup_done(bool ok) {   // false if any device's setup failed
-        std::unique_lock<std::mutex> l(m);
-        if (!ok) setup_failed = true;
-        if (++arrived == world) cv.notify_all();
-        else cv.wait(l, [&] { return arrived == world; });
-        return !setup_failed;
-    }
-};
-
-// One device's communicator and its abort state (touched by that device's thread only).
-struct Link {
-    ncclComm_t comm = nullptr;
-    bool aborted = false;
-    Sync *sy = nullptr;
-    void abort() {
-        if (!aborted && comm) (void)ncclCommAbort(comm);
-        aborted = true;
-    }
-    // nonzero (and the communicator aborted) once any device has failed
-    int check() {
-        if (!sy->failed.load()) return 0;
-        abort();
-        return RT_E_INVALID;
-    }
-};
+// The abort protocol (setup barrier, shared failure flag, each device aborting only its own
+// communicator) lives in mgpu_protocol.h, free of HIP/RCCL types so that it is tested on the CPU.
+void comm_abort(ncclComm_t c) { (void)ncclCommAbort(c); }
+using Sync = rtamd_mgpu::Sync;
+using Link = rtamd_mgpu::LinkT<ncclComm_t, comm_abort>;
+using RunGuard = rtamd_mgpu::RunGuardT<Link>;
 
 // the renderer's abort poll (rtamd_renderer_set_poll): a tile exchange waits on this device's collective
 int link_poll(void *user) { return static_cast<Link *>(user)->check(); }
-
-// Scope guard of one device's run: arrives at the setup barrier as failed if the run ends before
-// setup(), and on an error after it raises the flag and aborts this device's communicator.
-struct RunGuard {
-    Sync &sy;
-    Link &ln;
-    bool arrived = false, ok = false;
-    bool setup() {
-        arrived = true;
-        return sy.setup_done(true);
-    }
-    // an error after setup: raise the flag and abort this device's communicator now, before the
-    // renderer and buffers are torn down (their teardown must not wait on a collective a peer is
-    // still blocked in); called by the resource guards' destructors, and again (a no-op) at scope exit
-    void fail_now() {
-        if (arrived && !ok) {
-            sy.failed = true;
-            ln.abort();
-        }
-    }
-    ~RunGuard() {
-        if (!arrived) (void)sy.setup_done(false);
-        else fail_now();
-    }
-};
 
 int hip_err(hipError_t e, const char *what) {
     return rtamd::fail(e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP,
@@ -173,13 +117,14 @@ bool injected_failure(int rank) {
 // Waits for stream s (which holds collectives) while watching the other devices: returns an error
 // (and aborts this device's communicator) if one of them failed.
 int wait_stream(hipStream_t s, Link &ln) {
-    for (;;) {
-        const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess) return RT_OK;
-        if (q != hipErrorNotReady) return hip_err(q, "hipStreamQuery");
-        if (ln.check()) return rtamd::fail(RT_E_INVALID, "another device of the render failed");
-        std::this_thread::yield();
-    }
+    hipError_t err = hipSuccess;
+    const rtamd_mgpu::WaitResult w = rtamd_mgpu::wait_watching([&] {
+        err = hipStreamQuery(s);
+        return err == hipSuccess ? 0 : err == hipErrorNotReady ? 1 : 2;
+    }, ln);
+    if (w == rtamd_mgpu::kDone) return RT_OK;
+    if (w == rtamd_mgpu::kOwnError) return hip_err(err, "hipStreamQuery");
+    return rtamd::fail(RT_E_INVALID, "another device of the render failed");
 }
 #define MWAIT(s)                                   \
     do {                                           \
