@@ -2333,6 +2333,24 @@ struct rt_renderer {
                         }
                         if (k == 0) launch_ms.push_back(t1 >= t0 && t0 != ~0ull ? (double)(t1 - t0) / wall_khz : 0.0);
                     }
+                if (std::getenv("RTAMD_TIMELINE")) {
+                    // diagnostic: every pass's trace launches on the device clock, ms from the run's first
+                    // trace start -- "pass k: start of bounce 0, 1, 2 | end of the last bounce"
+                    auto span = [&](int k, int b, int end) {
+                        const unsigned long long *w = &sp[((size_t)k * (bounces + 1) + b) * kSpanWords];
+                        unsigned long long t = end ? 0 : ~0ull;
+                        for (int x = 0; x < kSpanSlots; x++) t = end ? std::max(t, w[kSpanSlots + x]) : std::min(t, w[x]);
+                        return t;
+                    };
+                    unsigned long long base = ~0ull;
+                    for (int k = 0; k < count; k++) base = std::min(base, span(k, 0, 0));
+                    for (int k = 0; k < count; k++) {
+                        std::fprintf(stderr, "timeline pass %d:", k);
+                        for (int b = 0; b < std::min(bounces, 3); b++)
+                            std::fprintf(stderr, " %.2f", (double)(span(k, b, 0) - base) / wall_khz);
+                        std::fprintf(stderr, " | %.2f\n", (double)(span(k, bounces - 1, 1) - base) / wall_khz);
+                    }
+                }
                 // live rays per bounce of the first pass: its context's live counts (valid when that
                 // pass was the context's last, i.e. runs of at most `inflight` passes)
                 launch_live.resize((size_t)bounces + 1);

@@ -189,3 +189,20 @@ def test_multi_device_rejects_bad_device_lists(gpu):
         R.render(psc, devices=[0, R.device_count()])
     with pytest.raises(R.RtError, match="whole frame"):
         R.render(psc, devices=[0], pass_begin=1)
+
+
+@pytest.mark.parametrize("sort", [True, False])
+def test_renderer_reuse_bitexact(gpu, sort):
+    """A renderer reused across runs -- first the short remainder pass (5 rays per pixel), then the whole
+    frame twice -- renders the frame exactly as the oracle does each time (no state carried between
+    runs: live counts, trace queues, reorder counts and per-pass buffers are reset per pass)."""
+    image = (96, 54, 45, 16)
+    osc, psc = _pair("teapot", image)
+    ofb, _ = osc.render(sort=sort)
+    r = R.Renderer(psc, sort=sort)
+    r.run(pass_begin=2, count=1)
+    for _ in range(2):
+        r.clear()
+        r.run(pass_begin=0, count=-1)
+        fb = r.framebuffer()
+        assert np.array_equal(fb, ofb), _diff(fb, ofb)
