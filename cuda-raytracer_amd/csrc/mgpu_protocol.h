@@ -1,5 +1,5 @@
 // mgpu_protocol.h — the multi-device abort protocol of rt_multi.hip, free of HIP and RCCL types so
-// that it can be tested on the CPU (tests/cpp/mgpu_protocol_test.cpp, tests/test_mgpu_protocol.py).
+// that it can be tested on the CPU (tests/native/mgpu_protocol_test.cpp, tests/test_mgpu_protocol.py).
 //
 // A device that fails must not leave its peers blocked in a collective.  Every device first builds
 // its renderer and buffers (where nearly every failure happens: out of memory, a bad scene) and

@@ -50,6 +50,8 @@ int fail(int code, const std::string &msg);
 extern "C" int rtamd_renderer_set_poll(rt_renderer *r, int (*fn)(void *), void *user);   // rt_render.hip
 extern "C" int rtamd_renderer_run_pitched(rt_renderer *r, int pass_begin, int count, int stride,
                                           float *d_pass_sums, size_t pitch, rt_stats *stats);   // rt_render.hip
+extern "C" int rtamd_renderer_run_async_pitched(rt_renderer *r, int pass_begin, int count, int stride,
+                                                float *d_pass_sums, size_t pitch);             // rt_render.hip
 
 namespace {
 
@@ -75,6 +77,26 @@ struct DevState {
     rt_stats stats{};
     double exchange_ms = 0;
 };
+
+void add_stats(DevState &st, const rt_stats &s) {
+    st.stats.live_segments += s.live_segments;
+    st.stats.generated_rays += s.generated_rays;
+    st.stats.sorted_items += s.sorted_items;
+    st.stats.nodes_popped += s.nodes_popped;
+    st.stats.internal_visits += s.internal_visits;
+    st.stats.triangle_tests += s.triangle_tests;
+    st.stats.sphere_tests += s.sphere_tests;
+    st.stats.hits += s.hits;
+    st.stats.misses += s.misses;
+    st.stats.hits_sphere += s.hits_sphere;
+    st.stats.dead_slots += s.dead_slots;
+    st.stats.passes += s.passes;
+    st.stats.kernel_ms += s.kernel_ms;
+    st.stats.process_ms += s.process_ms;
+    st.stats.sort_ms += s.sort_ms;
+    st.stats.trace_ms += s.trace_ms;
+    st.stats.trace_launches += s.trace_launches;
+}
 
 // The abort protocol (setup barrier, shared failure flag, each device aborting only its own
 // communicator) lives in mgpu_protocol.h, free of HIP/RCCL types so that it is tested on the CPU.
@@ -179,43 +201,59 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
     if (!run.setup()) return rtamd::fail(RT_E_INVALID, "another device of the render failed");
     if (injected_failure(st.rank)) return rtamd::fail(RT_E_INVALID, "injected failure (RTAMD_FAIL_AFTER_SETUP)");
     using clk = std::chrono::high_resolution_clock;
+    // Overlapped exchange (the default; RTAMD_XCHG_OVERLAP=0: one exchange after each chunk's render):
+    // the chunk's passes are enqueued without waiting (rt_renderer_run_async), and the exchange
+    // stream takes the slices of every `xr` rounds as soon as this device's passes of those rounds
+    // have written their sums (rt_renderer_wait_pass), while the later passes still render.  The
+    // exchange order -- rounds, then the owners' ascending pass order in add_slices_kernel -- is the
+    // synchronous one, so the image is the same bit for bit.  Every device issues the same sequence
+    // of collectives (it depends only on R, chunk and xr).
+    const char *ov = std::getenv("RTAMD_XCHG_OVERLAP");
+    const bool overlap = !ov || std::atoi(ov) != 0;
+    const char *xre = std::getenv("RTAMD_XCHG_ROUNDS");
+    const int xr = overlap ? std::max(1, xre ? std::atoi(xre) : 4) : chunk;
     for (int k0 = 0; k0 < R; k0 += chunk) {
         const int m = std::min(chunk, R - k0);
         // this device's passes of rounds k0 .. k0+m-1
         const int first = st.rank + world * k0;
         const int mine = first < P ? std::min(m, (P - 1 - first) / world + 1) : 0;
-        if (mine > 0) {
+        if (mine > 0 && overlap) {
+            rc = rtamd_renderer_run_async_pitched(ren, first, mine, world, buf, pitch);
+            if (rc) return rc;
+        }
+        if (mine > 0 && !overlap) {
             rt_stats s{};
             rc = rtamd_renderer_run_pitched(ren, first, mine, world, buf, pitch, &s);
             if (rc) return rc;
-            st.stats.live_segments += s.live_segments;
-            st.stats.generated_rays += s.generated_rays;
-            st.stats.sorted_items += s.sorted_items;
-            st.stats.nodes_popped += s.nodes_popped;
-            st.stats.internal_visits += s.internal_visits;
-            st.stats.triangle_tests += s.triangle_tests;
-            st.stats.sphere_tests += s.sphere_tests;
-            st.stats.hits += s.hits;
-            st.stats.misses += s.misses;
-            st.stats.hits_sphere += s.hits_sphere;
-            st.stats.dead_slots += s.dead_slots;
-            st.stats.passes += s.passes;
-            st.stats.kernel_ms += s.kernel_ms;
-            st.stats.process_ms += s.process_ms;
-            st.stats.sort_ms += s.sort_ms;
-            st.stats.trace_ms += s.trace_ms;
-            st.stats.trace_launches += s.trace_launches;
+            add_stats(st, s);
         }
         // rounds of the chunk where this device has no pass send stale rows, which the owners'
         // adds skip (pass src + N*k does not exist)
-        const auto t0 = clk::now();
-        MNCCL(ncclGroupStart());
-        for (int j = 0; j < m; j++)
-            MNCCL(ncclAllToAll(buf + (size_t)j * pitch, recv + (size_t)j * pitch, sl, ncclFloat32, comm, g.s));
-        MNCCL(ncclGroupEnd());
-        hipLaunchKernelGGL(add_slices_kernel, dim3((unsigned)((sl + 255) / 256)), dim3(256), 0, g.s, slice, recv, sl,
-                           world, m, k0, P);
-        MHIP(hipGetLastError());
+        auto t0 = clk::now();
+        for (int j0 = 0; j0 < m; j0 += xr) {
+            const int j1 = std::min(m, j0 + xr);
+            if (overlap)
+                for (int j = j0; j < std::min(j1, mine); j++) {
+                    rc = rt_renderer_wait_pass(ren, j, g.s);
+                    if (rc) return rc;
+                }
+            MNCCL(ncclGroupStart());
+            for (int j = j0; j < j1; j++)
+                MNCCL(ncclAllToAll(buf + (size_t)j * pitch, recv + (size_t)j * pitch, sl, ncclFloat32, comm, g.s));
+            MNCCL(ncclGroupEnd());
+            hipLaunchKernelGGL(add_slices_kernel, dim3((unsigned)((sl + 255) / 256)), dim3(256), 0, g.s, slice,
+                               recv + (size_t)j0 * pitch, sl, world, j1 - j0, k0 + j0, P);
+            MHIP(hipGetLastError());
+        }
+        if (mine > 0 && overlap) {
+            // the passes render on the renderer's own streams, which no collective waits behind:
+            // this wait ends even if a peer device has failed
+            rt_stats s{};
+            rc = rt_renderer_finish(ren, &s);
+            if (rc) return rc;
+            add_stats(st, s);
+            t0 = clk::now();            // exchange_ms: what the render did not hide
+        }
         // the next chunk's render overwrites buf: the exchange must have read it
         MWAIT(g.s);
         st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();

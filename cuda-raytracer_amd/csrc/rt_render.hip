@@ -64,6 +64,9 @@ namespace {
 #ifndef RT_QUEUES
 #define RT_QUEUES 8
 #endif
+#ifndef RT_XCDA
+#define RT_XCDA 1                     // XCD-affine trace order compiled in (xcda_map; RTAMD_XCDA picks the bounces)
+#endif
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 constexpr int kStackLds = RT_STACK_LDS; // stack entries per lane kept in LDS (deeper: global)
 constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138)
@@ -146,7 +149,7 @@ struct DevScene {
 
 #ifdef RT_PROFILE
 // Wave-level traversal profile (debug builds only): see tools/variants.sh + RT_PROFILE=1.
-__device__ unsigned long long g_prof[2][12];   // [bounce 0, later bounces]
+__device__ unsigned long long g_prof[2][14];   // [bounce 0, later bounces]
 #define PROF(i, v) (prof[i] += (v))
 #else
 #define PROF(i, v) ((void)0)
@@ -318,12 +321,46 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #define RT_SORT_GRID 0                // cap on the reorder's hist/scatter grid (0: 8 blocks per CU)
 #endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8)))
+
+// XCD-affine trace order of a sorted bounce (xtot = the reorder's 65 bucket totals).  After the
+// stable reorder the live slots are the 64 live buckets back to back, each holding its rays in the
+// previous slot order -- at bounce 1, pixel order -- so an equal split of the slot range gives every
+// XCD group eight whole buckets, i.e. rays from the whole image, and every XCD's 4 MB L2 sweeps the
+// whole scene.  Here queue shard x owns the x-th eighth of EVERY bucket instead,
+//   [off_b + len_b * x / 8, off_b + len_b * (x + 1) / 8)  for b = 0..63,
+// which at bounce 1 is the x-th band of image rows: an XCD's rays start on the surfaces of one band.
+// The shard's queue word counts a virtual index c over those sub-ranges back to back; this maps c to
+// its slot and the number of slots left in c's sub-range (false: c is past the shard's end).  The
+// slots (and so seeds and hit records) are unchanged; only which workgroups trace them changes, and
+// each sub-range is contiguous, so ray loads and hit stores stay coalesced.  Lane b holds bucket b.
+__device__ __forceinline__ bool xcda_map(const uint32_t *__restrict__ xtot, uint32_t x, uint32_t c, uint32_t &slot,
+                                         uint32_t &avail) {
+    const uint32_t lane = lane_id();
+    const uint32_t len = xtot[lane];
+    const uint32_t lo = (uint32_t)(((uint64_t)len * x) / kQueues);
+    const uint32_t sub = (uint32_t)(((uint64_t)len * (x + 1)) / kQueues) - lo;
+    uint32_t off = len, cum = sub;      // inclusive scans over the buckets
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const uint32_t a = __shfl_up(off, k), b = __shfl_up(cum, k);
+        if (lane >= (uint32_t)k) { off += a; cum += b; }
+    }
+    const uint32_t b = (uint32_t)__popcll(__ballot(cum <= c));   // cum is non-decreasing: a prefix of lanes
+    if (b >= 64) return false;
+    const uint32_t cum_b = __builtin_amdgcn_readlane(cum, b);
+    const uint32_t start_b = __builtin_amdgcn_readlane(off - len + lo, b);   // bucket start + shard offset
+    const uint32_t sub_b = __builtin_amdgcn_readlane(sub, b);
+    slot = start_b + (c - (cum_b - sub_b));
+    avail = cum_b - c;
+    return true;
+}
 template <bool SORTED, bool COUNT, int FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
-                                                       unsigned long long *__restrict__ tspan) {
+                                                       unsigned long long *__restrict__ tspan,
+                                                       const uint32_t *__restrict__ xtot) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
@@ -347,7 +384,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     // The live range is split into kQueues equal segments, each with its own queue word; a wave
     // starts on the segment of its XCD group (blockIdx % 8) and moves on when that one is drained.
     uint32_t shard = blockIdx.x % kQueues, tried = 0;
-    uint32_t q_next = 0, q_end = 0;     // this wave's current chunk (wave-uniform)
+    uint32_t q_next = 0, q_end = 0;     // this wave's current slot run (wave-uniform)
+    uint32_t v_next = 0, v_end = 0;     // xtot: the rest of its chunk in the shard's virtual index space
+    constexpr bool kXcda = RT_XCDA && SORTED && FIRST == 0;   // xtot is passed for sorted later bounces only
     bool exhausted = false;
     int slot = -1;                      // < 0: lane has no ray
     V3 o{0, 0, 0}, d{0, 0, 0};
@@ -359,7 +398,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     int ti = 0, te = 0;                 // the lane is in a leaf while ti < te
     unsigned pn = 0, iv = 0, tt = 0, nlive = 0;
 #ifdef RT_PROFILE
-    unsigned long long prof[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long prof[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     // One internal node's step (both children's slabs, scene.cu:196-225) on the record {a, b, c, kids}:
     // pushes the near child when both are hit, enters the next one; returns whether the lane needs
@@ -479,18 +518,38 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             bool fresh = false;
             while (idle && !exhausted) {
                 if (q_next >= q_end) {
-                    const uint32_t seg_lo = (uint32_t)(((uint64_t)L * shard) / kQueues);
-                    const uint32_t seg_hi = (uint32_t)(((uint64_t)L * (shard + 1)) / kQueues);
-                    uint32_t c = 0;
-                    if (lane_id() == 0) c = atomicAdd(queue + shard * kQueueStride, chunk);
-                    c = __builtin_amdgcn_readfirstlane(__shfl(c, 0)) + seg_lo;
-                    if (c >= seg_hi) {
-                        shard = (shard + 1) % kQueues;
-                        if (++tried == kQueues) exhausted = true;
-                        continue;
+                    uint32_t c = v_next;
+                    if (!kXcda || v_next >= v_end) {      // a new chunk of the shard
+                        c = 0;
+                        if (lane_id() == 0) c = atomicAdd(queue + shard * kQueueStride, chunk);
+                        c = __builtin_amdgcn_readfirstlane(__shfl(c, 0));
+                        v_end = c + chunk;
                     }
-                    q_next = c;
-                    q_end = min(c + chunk, seg_hi);
+                    if (kXcda && xtot) {
+                        uint32_t s0, avail;
+                        if (!xcda_map(xtot, shard, c, s0, avail)) {
+                            v_next = v_end = 0;
+                            shard = (shard + 1) % kQueues;
+                            if (++tried == kQueues) exhausted = true;
+                            continue;
+                        }
+                        const uint32_t n = min(v_end - c, avail);
+                        q_next = s0;
+                        q_end = s0 + n;
+                        v_next = c + n;
+                    } else {
+                        const uint32_t seg_lo = (uint32_t)(((uint64_t)L * shard) / kQueues);
+                        const uint32_t seg_hi = (uint32_t)(((uint64_t)L * (shard + 1)) / kQueues);
+                        c += seg_lo;
+                        if (kXcda) v_next = v_end;
+                        if (c >= seg_hi) {
+                            shard = (shard + 1) % kQueues;
+                            if (++tried == kQueues) exhausted = true;
+                            continue;
+                        }
+                        q_next = c;
+                        q_end = min(c + chunk, seg_hi);
+                    }
                 }
                 const uint32_t avail = q_end - q_next;
                 const uint32_t r = rank_below(idle);
@@ -558,6 +617,14 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             const bool mixed = lf != 0 && (act & ~lf) != 0;
             PROF(8, mixed);
             if (mixed) PROF(9, min(__popcll(lf), __popcll(act & ~lf)));
+            // steps whose active lanes all read one record (a scalar load could serve them), and
+            // steps where at least 3/4 of the active lanes read the first active lane's record
+            const uintptr_t ra = slot >= 0 ? (uintptr_t)(ti < te ? S.tris + (size_t)ti * 3 : S.nodes + (size_t)ref * 4) : 0;
+            const int first = __builtin_ctzll(act);
+            const uintptr_t r0 = ((uintptr_t)__shfl((unsigned)(ra >> 32), first) << 32) | __shfl((unsigned)ra, first);
+            const unsigned long long same = __ballot(slot >= 0 && ra == r0);
+            PROF(12, same == act);
+            PROF(13, 4 * __popcll(same) >= 3 * __popcll(act));
         }
 #endif
         if (slot < 0) continue;
@@ -621,7 +688,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 #ifdef RT_PROFILE
     prof[11] = wave_sum((unsigned)prof[10]);   // pop iterations summed over the lanes
     if (lane_id() == 0)
-        for (int i = 0; i < 12; i++)
+        for (int i = 0; i < 14; i++)
             if (i != 10) atomicAdd(&g_prof[FIRST ? 0 : 1][i], prof[i]);
 #endif
 }
@@ -1415,6 +1482,8 @@ struct rt_renderer {
     // shade/reorder (INLINE), saving the hit round trip and the trace launch per bounce.
     bool inline_hits = false;
     int fused_upto = -1;              // fused reorder at bounces <= this (when not `fused`)
+    // XCD-affine trace order (xcda_map) at sorted bounces 1..xcda_upto; RTAMD_XCDA overrides (0: off)
+    int xcda_upto = std::getenv("RTAMD_XCDA") ? std::atoi(std::getenv("RTAMD_XCDA")) : 1;
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
     DevBuf<float4> spheres, tris, mats, nodes;
@@ -1731,11 +1800,13 @@ struct rt_renderer {
             uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
             const bool last = b + 1 == bounces;
             uint32_t *hist = shade_hist && !last ? c.sort_counts.p : nullptr;   // the shade kernel counts the buckets
+            // XCD-affine trace order (xcda_map) at the sorted bounces 1..xcda_upto: the previous reorder's totals
+            const uint32_t *xt = sort && b >= 1 && b <= xcda_upto ? c.sort_totals.p : nullptr;
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr); \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr, xt); \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
@@ -1897,13 +1968,13 @@ struct rt_renderer {
     do {                                                                                                           \
         if (b == 0) {                                                                                              \
             hipLaunchKernelGGL((trace_kernel<true, COUNT, 2>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr, nullptr);              \
             hipLaunchKernelGGL((shade_kernel<true, COUNT, 2, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
                                pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
                                seed_term, last, ctr.p, nullptr);                                                   \
         } else {                                                                                                   \
             hipLaunchKernelGGL((trace_kernel<true, COUNT, 0>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr, nullptr);              \
             hipLaunchKernelGGL((shade_kernel<true, COUNT, 0, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
                                pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
                                seed_term, last, ctr.p, c.gslot[cur].p);                                            \
@@ -2026,10 +2097,10 @@ struct rt_renderer {
         const int tgrid = std::min(blocks_for(n), trace_blocks);
         if (counters)
             hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr);
+                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr, nullptr);
         else
             hipLaunchKernelGGL((trace_kernel<false, false, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr);
+                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr, nullptr);
         HIPCHK(hipGetLastError());
         std::vector<float2> h((size_t)n);
         HIPCHK(hipMemcpyAsync(h.data(), hits.p, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, s0));
@@ -2056,27 +2127,41 @@ struct rt_renderer {
     // A run that failed (or was aborted because a peer device failed) may leave collectives of this
     // renderer's communicator pending: the destructor then aborts the communicator instead of waiting
     // for its streams (which could block forever) and destroying it.
+    // Set only where work (and so collectives) may have been enqueued: argument errors and misuse of
+    // the async calls leave it alone, and a run that finishes cleanly clears it.
     bool failed = false;
+    bool enqueued = false;            // run_impl got past validation (set per call)
     int run(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st, size_t pitch = 0) {
+        if (run_pending) return rtamd::fail(RT_E_INVALID, "rt_renderer_run: an async run is not finished");
         int rc = run_impl(pass_begin, count, stride, pass_sums, st, pitch, false);
         if (!rc) rc = finish_run(st);
-        if (rc) failed = true;
+        if (rc && enqueued) failed = true;
+        if (!rc) failed = false;
         return rc;
     }
     // rt_renderer_run_async: the same passes enqueued, nothing waited for; pass k's sums are complete at
-    // pass_done[k] (rt_renderer_wait_pass), the run at finish_run (rt_renderer_finish)
+    // pass_done[k] (rt_renderer_wait_pass), the run at finish_run (rt_renderer_finish).  Everything
+    // finish_run reads is the state the run was enqueued with (run_*), not the renderer's current
+    // settings, and the calls that would change that state or touch the framebuffer are refused
+    // while the run is pending (busy()).
     bool run_pending = false;
     int run_count = 0, run_inflight = 0;
+    bool run_events = false, run_tsort = false, run_inline = false;
+    size_t run_span_words = 0;        // words of tspans the run's passes wrote
     int64_t run_sorted = 0, run_generated = 0;
     std::chrono::high_resolution_clock::time_point run_w0;
     double run_enq_ms = 0;
     std::vector<hipEvent_t> pass_done;
-    int run_async(int pass_begin, int count, int stride, float *pass_sums) {
+    int busy(const char *what) const {
+        return run_pending ? rtamd::fail(RT_E_INVALID, std::string(what) + ": an async run is not finished (rt_renderer_finish)")
+                           : RT_OK;
+    }
+    int run_async(int pass_begin, int count, int stride, float *pass_sums, size_t pitch = 0) {
         if (run_pending) return rtamd::fail(RT_E_INVALID, "rt_renderer_run_async: the previous run is not finished");
         if (!pass_sums) return rtamd::fail(RT_E_INVALID, "rt_renderer_run_async: the pass sums buffer is required");
         if (tsort()) return rtamd::fail(RT_E_INVALID, "rt_renderer_run_async: not for pixel tiles with sort on");
-        const int rc = run_impl(pass_begin, count, stride, pass_sums, nullptr, 0, true);
-        if (rc) failed = true;
+        const int rc = run_impl(pass_begin, count, stride, pass_sums, nullptr, pitch, true);
+        if (rc && enqueued) failed = true;
         return rc;
     }
     // Waits for everything queued on c's stream; with an abort poll (multi-device tile renders) the
@@ -2091,12 +2176,17 @@ struct rt_renderer {
     }
     int run_impl(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st, size_t pitch, bool async) {
         const auto w0 = std::chrono::high_resolution_clock::now();
+        enqueued = false;
         HIPCHK(hipSetDevice(device));
         if (stride < 1) stride = 1;
         const int P = pass_count();
         if (count < 0) count = pass_begin < P ? (P - pass_begin + stride - 1) / stride : 0;
         if (pass_begin < 0 || (count > 0 && pass_begin + (int64_t)(count - 1) * stride >= P))
             return rtamd::fail(RT_E_INVALID, "pass range outside the render");
+        if (tsort() && !xfn)
+            return rtamd::fail(RT_E_INVALID, "pixel tiles with sort on need the per-bounce exchange "
+                                             "(rt_renderer_set_exchange)");
+        enqueued = true;
         const int inflight = std::min(nctx, std::max(1, P));
         {   // the trace grid of this run, for the passes it actually keeps in flight
             const int concurrent = std::max(1, std::min(inflight, count));
@@ -2133,8 +2223,6 @@ struct rt_renderer {
             return pass_sums ? pass_sums + (size_t)k * (pitch ? pitch : (size_t)px3) : c.psum.p;
         };
         if (tsort()) {
-            if (!xfn) return rtamd::fail(RT_E_INVALID, "pixel tiles with sort on need the per-bounce exchange "
-                                                       "(rt_renderer_set_exchange)");
             // staggered first passes: context j starts at step j * bounces / inflight (RTAMD_TSTAGGER=0:
             // all at step 0, i.e. the passes of a group advance together)
             const char *stg = std::getenv("RTAMD_TSTAGGER");
@@ -2246,6 +2334,10 @@ struct rt_renderer {
         run_pending = true;
         run_count = count;
         run_inflight = inflight;
+        run_events = pass_events;
+        run_tsort = tsort();
+        run_inline = inline_hits;
+        run_span_words = pass_events ? (size_t)count * kSpanWords * (bounces + 1) : 0;
         run_sorted = sorted;
         run_generated = generated;
         run_w0 = w0;
@@ -2258,6 +2350,7 @@ struct rt_renderer {
         run_pending = false;
         HIPCHK(hipSetDevice(device));
         const int count = run_count, inflight = run_inflight;
+        const bool events = run_events, tsorted = run_tsort, inl = run_inline;
         const int64_t sorted = run_sorted, generated = run_generated;
         const auto w0 = run_w0;
         if (int rc = wait_event(t_end)) return rc;    // abortable when a peer device can fail
@@ -2266,16 +2359,16 @@ struct rt_renderer {
                          std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - w0).count());
 #ifdef RT_PROFILE
         {
-            unsigned long long pr[2][12];
+            unsigned long long pr[2][14];
             HIPCHK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof(pr)));
             for (int f = 0; f < 2; f++) {
                 const unsigned long long *q = pr[f];
                 const double it = (double)std::max(1ull, q[0]);
                 std::fprintf(stderr, "RT_PROFILE %s wave_iters %llu active/iter %.2f leaf/iter %.2f iters_with_leaf %.3f "
                              "iters_with_inner %.3f iters_with_pop %.3f refills/iter %.3f idle_iters %llu mixed %.3f "
-                             "minority/mixed %.2f lane_pops/iter %.3f\n",
+                             "minority/mixed %.2f lane_pops/iter %.3f uniform_record %.3f three_quarters_same %.3f\n",
                              f ? "later" : "bounce0", q[0], q[1] / it, q[2] / it, q[3] / it, q[4] / it, q[5] / it,
-                             q[6] / it, q[7], q[8] / it, q[9] / (double)std::max(1ull, q[8]), q[11] / it);
+                             q[6] / it, q[7], q[8] / it, q[9] / (double)std::max(1ull, q[8]), q[11] / it, q[12] / it, q[13] / it);
             }
             std::memset(pr, 0, sizeof(pr));
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));
@@ -2297,7 +2390,7 @@ struct rt_renderer {
             // (reorder begin, end) pairs between them, in enqueue order.
             double proc = 0, srt = 0, trc = 0;
             uint64_t trace_launches = 0;
-            for (int q = 0; pass_events && !tsort() && q < inflight; q++) {
+            for (int q = 0; events && !tsorted && q < inflight; q++) {
                 const int passes_here = count > q ? (count - q + inflight - 1) / inflight : 0;
                 size_t e = 0;
                 for (int r = 0; r < passes_here; r++)
@@ -2316,8 +2409,8 @@ struct rt_renderer {
             // wave's end (the stream's events would add the queueing before the first wave)
             launch_ms.clear();
             launch_live.clear();
-            if (pass_events && !inline_hits && !tsort() && count > 0) {
-                std::vector<unsigned long long> sp((size_t)count * kSpanWords * (bounces + 1));
+            if (events && !inl && !tsorted && count > 0 && run_span_words <= tspans.n) {
+                std::vector<unsigned long long> sp(run_span_words);
                 HIPCHK(hipMemcpy(sp.data(), tspans.p, sp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
                 for (int k = 0; k < count; k++)
                     for (int b = 0; b < bounces; b++) {
@@ -2351,16 +2444,18 @@ struct rt_renderer {
                         std::fprintf(stderr, " | %.2f\n", (double)(span(k, bounces - 1, 1) - base) / wall_khz);
                     }
                 }
-                // live rays per bounce of the first pass: its context's live counts (valid when that
-                // pass was the context's last, i.e. runs of at most `inflight` passes)
-                launch_live.resize((size_t)bounces + 1);
-                HIPCHK(hipMemcpy(launch_live.data(), ctx[0].live.p, launch_live.size() * sizeof(uint32_t),
-                                 hipMemcpyDeviceToHost));
+                // live rays per bounce of the first pass: its context's live counts, which are pass 0's
+                // only when that pass was the context's last (runs of at most `inflight` passes);
+                // otherwise they are reported as 0 (unknown), not as a later pass's counts
+                launch_live.assign((size_t)bounces + 1, 0u);
+                if (count <= inflight)
+                    HIPCHK(hipMemcpy(launch_live.data(), ctx[0].live.p, launch_live.size() * sizeof(uint32_t),
+                                     hipMemcpyDeviceToHost));
                 launch_live.resize((size_t)bounces);
             }
             st->process_ms = proc;
             st->sort_ms = srt;
-            st->trace_ms = inline_hits ? 0.0 : trc;
+            st->trace_ms = inl ? 0.0 : trc;
             st->trace_launches = trace_launches;
             st->generated_rays = (uint64_t)generated;
             st->live_segments = c.live;
@@ -2482,6 +2577,13 @@ int rtamd_renderer_run_pitched(rt_renderer *r, int pass_begin, int count, int st
     return r->run(pass_begin, count, stride, d_pass_sums, stats, pitch);
 }
 
+// rt_multi.hip's overlapped exchange: rt_renderer_run_async into padded pass rows (pitch floats apart)
+int rtamd_renderer_run_async_pitched(rt_renderer *r, int pass_begin, int count, int stride, float *d_pass_sums,
+                                     size_t pitch) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    return r->run_async(pass_begin, count, stride, d_pass_sums, pitch);
+}
+
 int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride, float *d_pass_sums,
                     rt_stats *stats) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
@@ -2491,6 +2593,7 @@ int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t s
 int rt_renderer_run_host(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride, float *host_pass_sums,
                          rt_stats *stats) {
     if (!r || !host_pass_sums || count < 1) return rtamd::fail(RT_E_INVALID, "rt_renderer_run_host: bad argument");
+    if (int rc = r->busy("rt_renderer_run_host")) return rc;
     HIPCHK(hipSetDevice(r->device));
     const size_t bytes = (size_t)count * r->width * r->height * 3 * sizeof(float);
     float *d = nullptr;
@@ -2506,6 +2609,7 @@ int rt_renderer_run_host(rt_renderer *r, int32_t pass_begin, int32_t count, int3
 
 int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out) {
     if (!r || !fb_out) return rtamd::fail(RT_E_INVALID, "null argument");
+    if (int rc = r->busy("rt_renderer_read_framebuffer")) return rc;
     HIPCHK(hipSetDevice(r->device));
     HIPCHK(hipMemcpyAsync(fb_out, r->fb.p, r->fb.n * sizeof(float), hipMemcpyDeviceToHost, r->stream()));
     HIPCHK(hipStreamSynchronize(r->stream()));
@@ -2514,6 +2618,7 @@ int rt_renderer_read_framebuffer(rt_renderer *r, float *fb_out) {
 
 int rt_renderer_copy_framebuffer(rt_renderer *r, float *d_out) {
     if (!r || !d_out) return rtamd::fail(RT_E_INVALID, "null argument");
+    if (int rc = r->busy("rt_renderer_copy_framebuffer")) return rc;
     HIPCHK(hipSetDevice(r->device));
     HIPCHK(hipMemcpyAsync(d_out, r->fb.p, r->fb.n * sizeof(float), hipMemcpyDeviceToDevice, r->stream()));
     HIPCHK(hipStreamSynchronize(r->stream()));
@@ -2522,6 +2627,7 @@ int rt_renderer_copy_framebuffer(rt_renderer *r, float *d_out) {
 
 int rt_renderer_clear(rt_renderer *r) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    if (int rc = r->busy("rt_renderer_clear")) return rc;
     HIPCHK(hipSetDevice(r->device));
     HIPCHK(hipMemsetAsync(r->fb.p, 0, r->fb.n * sizeof(float), r->stream()));
     HIPCHK(hipStreamSynchronize(r->stream()));
@@ -2530,6 +2636,7 @@ int rt_renderer_clear(rt_renderer *r) {
 
 int rt_renderer_set_event_timing(rt_renderer *r, int32_t enable) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    if (int rc = r->busy("rt_renderer_set_event_timing")) return rc;
     r->pass_events = enable != 0;
     return RT_OK;
 }
@@ -2550,13 +2657,15 @@ int rt_renderer_wait_pass(rt_renderer *r, int32_t k, void *hip_stream) {
 
 int rt_renderer_finish(rt_renderer *r, rt_stats *stats) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    if (!r->run_pending) return rtamd::fail(RT_E_INVALID, "rt_renderer_finish: no run in flight");   // misuse: not a failure
     const int rc = r->finish_run(stats);
-    if (rc) r->failed = true;
+    r->failed = rc != RT_OK;
     return rc;
 }
 
 int rt_renderer_launch_profile(rt_renderer *r, int32_t cap, double *trace_ms_out, uint32_t *live_out) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    if (int rc = r->busy("rt_renderer_launch_profile")) return rc;
     const int n = (int)std::min<size_t>(r->launch_ms.size(), (size_t)std::max(cap, 0));
     for (int b = 0; b < n; b++) {
         if (trace_ms_out) trace_ms_out[b] = r->launch_ms[b];
@@ -2621,6 +2730,7 @@ int rtamd_renderer_set_poll(rt_renderer *r, int (*fn)(void *), void *user) {
 
 int rt_renderer_set_counters(rt_renderer *r, int32_t enable) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    if (int rc = r->busy("rt_renderer_set_counters")) return rc;
     r->counters = enable != 0;
     return RT_OK;
 }

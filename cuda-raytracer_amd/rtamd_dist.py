@@ -100,33 +100,51 @@ class PassShardedFrame:
                     self.async_render.start(mine, out[:len(mine)])
                 else:
                     self.render_passes(mine, out[:len(mine)])
-            step = self.xrounds if self.async_render is not None else m
-            for s0 in range(0, m, step):
-                s1 = min(s0 + step, m)
-                mine_here = [j for j in range(s0, s1) if j < len(mine)]
-                if self.async_render is not None:
-                    for j in mine_here:         # passes in flight finish in any order: wait for each
-                        self.async_render.wait(j)
-                if mine_here and self.stage is not None:
-                    self.buf[mine_here[0]:mine_here[-1] + 1, :self.pixels3].copy_(
-                        self.stage[mine_here[0]:mine_here[-1] + 1])
-                n = s1 - s0
-                if N > 1:
-                    # send[d, j] = slice d of this rank's pass framebuffer of round ks[s0 + j]; every rank
-                    # issues the same sequence of exchanges (it depends only on m and the step)
-                    send = self.buf[s0:s1].view(n, N, sl).transpose(0, 1).contiguous()
-                    recv = self.torch.empty_like(send)
-                    self.dist.all_to_all_single(recv, send)
-                else:
-                    recv = self.buf[s0:s1].view(1, n, sl)
-                for j in range(n):
-                    for src in range(N):            # pass src + N*k: ascending pass order
-                        if src + N * ks[s0 + j] < self.passes:
-                            self.slice.add_(recv[src, j])
-            if mine and self.async_render is not None:
+            started = bool(mine) and self.async_render is not None
+            try:
+                self._exchange(ks, mine, m)
+            except BaseException:
+                if started:
+                    # drain the run even though its stats are lost: the renderer must not be left
+                    # with a run pending (every later start() would fail) or with passes still
+                    # writing into buf / stage while the caller handles the error
+                    try:
+                        self.async_render.finish()
+                    except Exception:
+                        pass
+                raise
+            if started:
                 self.async_render.finish()
             done += len(mine)
         return done
+
+    def _exchange(self, ks, mine, m):
+        """The exchange of one chunk: slices of the passes of rounds ks go to their owners, which add
+        them in pass order (every `exchange_rounds` rounds with async_render)."""
+        N, sl = self.world, self.sl
+        step = self.xrounds if self.async_render is not None else m
+        for s0 in range(0, m, step):
+            s1 = min(s0 + step, m)
+            mine_here = [j for j in range(s0, s1) if j < len(mine)]
+            if self.async_render is not None:
+                for j in mine_here:         # passes in flight finish in any order: wait for each
+                    self.async_render.wait(j)
+            if mine_here and self.stage is not None:
+                self.buf[mine_here[0]:mine_here[-1] + 1, :self.pixels3].copy_(
+                    self.stage[mine_here[0]:mine_here[-1] + 1])
+            n = s1 - s0
+            if N > 1:
+                # send[d, j] = slice d of this rank's pass framebuffer of round ks[s0 + j]; every rank
+                # issues the same sequence of exchanges (it depends only on m and the step)
+                send = self.buf[s0:s1].view(n, N, sl).transpose(0, 1).contiguous()
+                recv = self.torch.empty_like(send)
+                self.dist.all_to_all_single(recv, send)
+            else:
+                recv = self.buf[s0:s1].view(1, n, sl)
+            for j in range(n):
+                for src in range(N):            # pass src + N*k: ascending pass order
+                    if src + N * ks[s0 + j] < self.passes:
+                        self.slice.add_(recv[src, j])
 
     def collect(self):
         """Gathers the owned slices to rank 0 (collective); returns rank 0's framebuffer."""

@@ -181,7 +181,10 @@ int rt_renderer_run(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t s
  * the k-th pass of the run (0-based) has written its sums, so the caller can exchange finished
  * passes while later ones render (the multi-GPU slice exchange); rt_renderer_finish waits for the
  * whole run and fills stats.  The framebuffer adds and every other rule are those of
- * rt_renderer_run.  No reference counterpart (the reference's gpu_raytrace returned at the end). */
+ * rt_renderer_run.  Until rt_renderer_finish returns, every other call on r that runs passes,
+ * touches the framebuffer or changes the run's settings (run, run_host, read/copy_framebuffer,
+ * clear, set_event_timing, set_counters, launch_profile) fails with RT_E_INVALID and changes
+ * nothing.  No reference counterpart (the reference's gpu_raytrace returned at the end). */
 int rt_renderer_run_async(rt_renderer *r, int32_t pass_begin, int32_t count, int32_t stride, float *d_pass_sums);
 int rt_renderer_wait_pass(rt_renderer *r, int32_t k, void *hip_stream);
 int rt_renderer_finish(rt_renderer *r, rt_stats *stats);
@@ -221,9 +224,9 @@ int rt_renderer_set_event_timing(rt_renderer *r, int32_t enable);
 /* Per trace launch of the last run's first pass (event timing on): trace_ms_out[b] = the launch's
  * device wall-clock span (first wave start to last wave end) and live_out[b] = the live rays it
  * traced, for bounce b < cap.  Returns the number of launches written (0 without event timing or
- * for scenes without triangles).  Live counts are that pass's when it was the last pass of its
- * context (runs of at most as many passes as are in flight: the benchmark's one-pass exclusive
- * run).  Measurement only; no reference counterpart. */
+ * for scenes without triangles).  Live counts are known only for runs of at most as many passes
+ * as are in flight (the benchmark's one-pass exclusive run); in a longer run live_out[b] is 0.
+ * Measurement only; no reference counterpart. */
 int rt_renderer_launch_profile(rt_renderer *r, int32_t cap, double *trace_ms_out, uint32_t *live_out);
 void rt_renderer_destroy(rt_renderer *r);
 

@@ -60,12 +60,25 @@ def test_async_run_misuse_is_refused(torch_gpu):
             ren.run_async(0, 2, 1, None)                    # the pass sums buffer is required
         with pytest.raises(R.RtError):
             ren.finish()                                    # nothing in flight
+        ren.set_event_timing(False)
         ren.run_async(0, 2, 1, out.data_ptr())
         with pytest.raises(R.RtError):
             ren.run_async(0, 2, 1, out.data_ptr())          # the previous run is not finished
         with pytest.raises(R.RtError):
             ren.wait_pass(2, torch.cuda.current_stream().cuda_stream)   # no pass 2 in this run
-        ren.finish()
+        # every call that would run passes, touch the framebuffer or change the pending run's
+        # settings is refused until finish() (finish used to read the current settings)
+        dev = torch.zeros(psc.pixels * 3, dtype=torch.float32, device="cuda")
+        for call in (lambda: ren.run(0, 1), lambda: ren.run_host(0, 1), ren.clear, ren.framebuffer,
+                     lambda: ren.copy_framebuffer(dev.data_ptr()), lambda: ren.set_event_timing(True),
+                     lambda: ren.set_counters(True), lambda: ren.launch_profile()):
+            with pytest.raises(R.RtError):
+                call()
+        st = ren.finish()                                   # the run's stats, with the run's (off) timing
+        assert st["passes"] == 2 and st["process_ms"] == 0.0
+        fb_async = ren.framebuffer()
+        np.testing.assert_array_equal(fb_async, out.sum(0).cpu().numpy())   # fb += pass sums, in order
+        ren.set_event_timing(True)
         with pytest.raises(R.RtError):
             ren.wait_pass(0, torch.cuda.current_stream().cuda_stream)   # the run is finished
         ren.run(0, 2)                                       # the renderer is usable again

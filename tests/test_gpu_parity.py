@@ -168,10 +168,16 @@ def test_fused_and_plain_reorder_bitexact(gpu, monkeypatch, scene, image, sort, 
 @pytest.mark.parametrize("scene,image,sort", [("cornell_plus", (40, 32, 350, 5), True),    # 18 passes: two chunks
                                               ("cornell", (33, 17, 190, 4), False),        # 10 passes, odd size
                                               ("teapot", (64, 36, 45, 16), True)])         # short last pass
-def test_multi_device_rccl_bitexact(gpu, scene, image, sort):
+@pytest.mark.parametrize("xchg", ["overlap", "overlap1", "sync"])
+def test_multi_device_rccl_bitexact(gpu, monkeypatch, scene, image, sort, xchg):
     """rt_render with rt_opts.device_count (in-library pass sharding over an RCCL communicator,
     slice all-to-all, ordered owner adds, gather to the first device) at N = 1, the only device
-    count this box has: bit-exact against the oracle and the single-device render."""
+    count this box has: bit-exact against the oracle and the single-device render.  The exchange
+    runs overlapped with the render (round 5: every 4 rounds, or every round) or after each chunk."""
+    if xchg == "sync":
+        monkeypatch.setenv("RTAMD_XCHG_OVERLAP", "0")
+    elif xchg == "overlap1":
+        monkeypatch.setenv("RTAMD_XCHG_ROUNDS", "1")
     osc, psc = _pair(scene, image)
     ofb, ost = osc.render(sort=sort)
     gfb, gst = R.render(psc, sort=sort, devices=[0])
