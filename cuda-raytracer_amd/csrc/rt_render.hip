@@ -64,9 +64,6 @@ namespace {
 #ifndef RT_QUEUES
 #define RT_QUEUES 8
 #endif
-#ifndef RT_XCDA
-#define RT_XCDA 1                     // XCD-affine trace order compiled in (xcda_map; RTAMD_XCDA picks the bounces)
-#endif
 constexpr int kBlock = 256;           // threads per workgroup (4 waves)
 constexpr int kStackLds = RT_STACK_LDS; // stack entries per lane kept in LDS (deeper: global)
 constexpr int kStackMax = 32;         // >= MAX_BVH_DEPTH + 1 (scene.cu:10, :138)
@@ -322,45 +319,12 @@ __device__ __forceinline__ void leaf_range(const DevScene &S, uint32_t ref, int 
 #endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE, RT_TRACE_WPE > 8 ? RT_TRACE_WPE : 8)))
 
-// XCD-affine trace order of a sorted bounce (xtot = the reorder's 65 bucket totals).  After the
-// stable reorder the live slots are the 64 live buckets back to back, each holding its rays in the
-// previous slot order -- at bounce 1, pixel order -- so an equal split of the slot range gives every
-// XCD group eight whole buckets, i.e. rays from the whole image, and every XCD's 4 MB L2 sweeps the
-// whole scene.  Here queue shard x owns the x-th eighth of EVERY bucket instead,
-//   [off_b + len_b * x / 8, off_b + len_b * (x + 1) / 8)  for b = 0..63,
-// which at bounce 1 is the x-th band of image rows: an XCD's rays start on the surfaces of one band.
-// The shard's queue word counts a virtual index c over those sub-ranges back to back; this maps c to
-// its slot and the number of slots left in c's sub-range (false: c is past the shard's end).  The
-// slots (and so seeds and hit records) are unchanged; only which workgroups trace them changes, and
-// each sub-range is contiguous, so ray loads and hit stores stay coalesced.  Lane b holds bucket b.
-__device__ __forceinline__ bool xcda_map(const uint32_t *__restrict__ xtot, uint32_t x, uint32_t c, uint32_t &slot,
-                                         uint32_t &avail) {
-    const uint32_t lane = lane_id();
-    const uint32_t len = xtot[lane];
-    const uint32_t lo = (uint32_t)(((uint64_t)len * x) / kQueues);
-    const uint32_t sub = (uint32_t)(((uint64_t)len * (x + 1)) / kQueues) - lo;
-    uint32_t off = len, cum = sub;      // inclusive scans over the buckets
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const uint32_t a = __shfl_up(off, k), b = __shfl_up(cum, k);
-        if (lane >= (uint32_t)k) { off += a; cum += b; }
-    }
-    const uint32_t b = (uint32_t)__popcll(__ballot(cum <= c));   // cum is non-decreasing: a prefix of lanes
-    if (b >= 64) return false;
-    const uint32_t cum_b = __builtin_amdgcn_readlane(cum, b);
-    const uint32_t start_b = __builtin_amdgcn_readlane(off - len + lo, b);   // bucket start + shard offset
-    const uint32_t sub_b = __builtin_amdgcn_readlane(sub, b);
-    slot = start_b + (c - (cum_b - sub_b));
-    avail = cum_b - c;
-    return true;
-}
 template <bool SORTED, bool COUNT, int FIRST>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S, PassArgs pa, const float4 *__restrict__ geo,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t *__restrict__ queue, float2 *__restrict__ hits,
                                                        uint32_t *__restrict__ overflow, Counters *__restrict__ ctr,
-                                                       unsigned long long *__restrict__ tspan,
-                                                       const uint32_t *__restrict__ xtot) {
+                                                       unsigned long long *__restrict__ tspan) {
     __shared__ uint2 stack[(kStackLds + 1) * kBlock];   // + one scratch entry per lane
     // tspan (per-launch timing, rt_renderer_set_event_timing): {first wave start, last wave end}
     // on the device's constant-rate wall clock, so a launch's duration excludes the queueing
@@ -384,9 +348,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
     // The live range is split into kQueues equal segments, each with its own queue word; a wave
     // starts on the segment of its XCD group (blockIdx % 8) and moves on when that one is drained.
     uint32_t shard = blockIdx.x % kQueues, tried = 0;
-    uint32_t q_next = 0, q_end = 0;     // this wave's current slot run (wave-uniform)
-    uint32_t v_next = 0, v_end = 0;     // xtot: the rest of its chunk in the shard's virtual index space
-    constexpr bool kXcda = RT_XCDA && SORTED && FIRST == 0;   // xtot is passed for sorted later bounces only
+    uint32_t q_next = 0, q_end = 0;     // this wave's current chunk (wave-uniform)
     bool exhausted = false;
     int slot = -1;                      // < 0: lane has no ray
     V3 o{0, 0, 0}, d{0, 0, 0};
@@ -518,38 +480,18 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
             bool fresh = false;
             while (idle && !exhausted) {
                 if (q_next >= q_end) {
-                    uint32_t c = v_next;
-                    if (!kXcda || v_next >= v_end) {      // a new chunk of the shard
-                        c = 0;
-                        if (lane_id() == 0) c = atomicAdd(queue + shard * kQueueStride, chunk);
-                        c = __builtin_amdgcn_readfirstlane(__shfl(c, 0));
-                        v_end = c + chunk;
+                    const uint32_t seg_lo = (uint32_t)(((uint64_t)L * shard) / kQueues);
+                    const uint32_t seg_hi = (uint32_t)(((uint64_t)L * (shard + 1)) / kQueues);
+                    uint32_t c = 0;
+                    if (lane_id() == 0) c = atomicAdd(queue + shard * kQueueStride, chunk);
+                    c = __builtin_amdgcn_readfirstlane(__shfl(c, 0)) + seg_lo;
+                    if (c >= seg_hi) {
+                        shard = (shard + 1) % kQueues;
+                        if (++tried == kQueues) exhausted = true;
+                        continue;
                     }
-                    if (kXcda && xtot) {
-                        uint32_t s0, avail;
-                        if (!xcda_map(xtot, shard, c, s0, avail)) {
-                            v_next = v_end = 0;
-                            shard = (shard + 1) % kQueues;
-                            if (++tried == kQueues) exhausted = true;
-                            continue;
-                        }
-                        const uint32_t n = min(v_end - c, avail);
-                        q_next = s0;
-                        q_end = s0 + n;
-                        v_next = c + n;
-                    } else {
-                        const uint32_t seg_lo = (uint32_t)(((uint64_t)L * shard) / kQueues);
-                        const uint32_t seg_hi = (uint32_t)(((uint64_t)L * (shard + 1)) / kQueues);
-                        c += seg_lo;
-                        if (kXcda) v_next = v_end;
-                        if (c >= seg_hi) {
-                            shard = (shard + 1) % kQueues;
-                            if (++tried == kQueues) exhausted = true;
-                            continue;
-                        }
-                        q_next = c;
-                        q_end = min(c + chunk, seg_hi);
-                    }
+                    q_next = c;
+                    q_end = min(c + chunk, seg_hi);
                 }
                 const uint32_t avail = q_end - q_next;
                 const uint32_t r = rank_below(idle);
@@ -1482,8 +1424,6 @@ struct rt_renderer {
     // shade/reorder (INLINE), saving the hit round trip and the trace launch per bounce.
     bool inline_hits = false;
     int fused_upto = -1;              // fused reorder at bounces <= this (when not `fused`)
-    // XCD-affine trace order (xcda_map) at sorted bounces 1..xcda_upto; RTAMD_XCDA overrides (0: off)
-    int xcda_upto = std::getenv("RTAMD_XCDA") ? std::atoi(std::getenv("RTAMD_XCDA")) : 1;
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
     DevBuf<float4> spheres, tris, mats, nodes;
@@ -1800,13 +1740,11 @@ struct rt_renderer {
             uint32_t *q = c.queue.p + (size_t)b * kQueues * kQueueStride;
             const bool last = b + 1 == bounces;
             uint32_t *hist = shade_hist && !last ? c.sort_counts.p : nullptr;   // the shade kernel counts the buckets
-            // XCD-affine trace order (xcda_map) at the sorted bounces 1..xcda_upto: the previous reorder's totals
-            const uint32_t *xt = sort && b >= 1 && b <= xcda_upto ? c.sort_totals.p : nullptr;
 #define RT_PROCESS3(SORTED, COUNT, FIRST)                                                                         \
     do {                                                                                                         \
         if (!inline_hits)                                                                                        \
             hipLaunchKernelGGL((trace_kernel<SORTED, COUNT, FIRST>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,    \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr, xt); \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, tspan ? tspan + kSpanWords * b : nullptr); \
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
@@ -1968,13 +1906,13 @@ struct rt_renderer {
     do {                                                                                                           \
         if (b == 0) {                                                                                              \
             hipLaunchKernelGGL((trace_kernel<true, COUNT, 2>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr, nullptr);              \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
             hipLaunchKernelGGL((shade_kernel<true, COUNT, 2, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
                                pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
                                seed_term, last, ctr.p, nullptr);                                                   \
         } else {                                                                                                   \
             hipLaunchKernelGGL((trace_kernel<true, COUNT, 0>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
-                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr, nullptr);              \
+                               c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
             hipLaunchKernelGGL((shade_kernel<true, COUNT, 0, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
                                pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
                                seed_term, last, ctr.p, c.gslot[cur].p);                                            \
@@ -2097,10 +2035,10 @@ struct rt_renderer {
         const int tgrid = std::min(blocks_for(n), trace_blocks);
         if (counters)
             hipLaunchKernelGGL((trace_kernel<false, true, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr, nullptr);
+                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr);
         else
             hipLaunchKernelGGL((trace_kernel<false, false, false>), dim3(tgrid), dim3(kBlock), 0, s0, ds, pa, geo.p,
-                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr, nullptr);
+                               live.p, queue.p, hits.p, overflow.p, ctr.p, nullptr);
         HIPCHK(hipGetLastError());
         std::vector<float2> h((size_t)n);
         HIPCHK(hipMemcpyAsync(h.data(), hits.p, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, s0));
