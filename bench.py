@@ -58,6 +58,7 @@ CONFIGS = {
     "cornell": ("cornell.scene", 256, 256, 64, 4, True, True),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+CPU_FULL_FRAME_S = 30.0  # cpu_baseline: frames estimated within this many seconds are timed whole
 TILE_ROWS = 8          # pixel-tile stripe height (--shard tiles; SURVEY §8e: interleaved 8-row stripes)
 
 
@@ -149,19 +150,28 @@ def cpu_baseline(cfg, args):
     threads = args.cpu_threads or env_threads or affinity
     scene, w, h, spp, bounces = cfg[:5]
     P = -(-spp // 20)
-    if P <= 4:
+    full = P <= 4
+    if not full:
+        first = run_cpu(exe, cfg, spp, 1, threads)                  # pass 0: 20 spp
+        # a frame that fits the sample budget is timed whole (cornell_plus: ~4 s on 16 threads)
+        full = first["seconds"] * P <= CPU_FULL_FRAME_S
+    if full:
         rec = run_cpu(exe, cfg, spp, -1, threads)
         secs, live = rec["seconds"], rec["live_segments"]
-        sample = "%s %dx%d %d spp %d bounces, the whole frame (%d passes): %.2f s" % (scene, w, h, spp, bounces, P, secs)
+        sample = "%s %dx%d %d spp %d bounces, the whole frame (%d passes) timed: %.2f s" % (scene, w, h, spp, bounces,
+                                                                                             P, secs)
     else:
-        first = run_cpu(exe, cfg, spp, 1, threads)                  # pass 0: 20 spp
         rem = spp - 20 * (P - 1)
         last = run_cpu(exe, cfg, rem, 1, threads)                   # the remainder pass (remaining = 0)
         secs = first["seconds"] * (P - 1) + last["seconds"]
         live = first["live_segments"] * (P - 1) + last["live_segments"]
-        sample = ("%s %dx%d %d bounces: first full 20-spp pass %.2f s + remainder %d-spp pass %.2f s, timed; "
-                  "frame of %d passes extrapolated linearly: %.1f s" % (scene, w, h, bounces, first["seconds"], rem,
-                                                                      last["seconds"], P, secs))
+        sample = ("%s %dx%d %d bounces: 2 of the frame's %d passes timed -- the first full 20-spp pass %.2f s and the "
+                  "remainder %d-spp pass %.2f s -- and the frame extrapolated linearly (passes are i.i.d. in cost, "
+                  "SURVEY 8(d)): %.1f s" % (scene, w, h, bounces, P, first["seconds"], rem, last["seconds"], secs))
+    if env_threads and not args.cpu_threads and env_threads < affinity:
+        sample += ("; %d threads, not all %d of the affinity mask: the GPU pool gives a one-GPU job a %d-CPU share "
+                   "(it sets OMP_NUM_THREADS=%d and asks jobs to size worker pools to it) although nproc shows the "
+                   "whole host" % (threads, affinity, env_threads, env_threads))
     return {
         "value": round(live / secs / 1e6, 3),
         "unit": "Mrays/s",
@@ -169,7 +179,7 @@ def cpu_baseline(cfg, args):
         "kind": "port",
         "sample": sample + " (oracle cpu_raytrace restatement, -O3 -ffast-math -fopenmp, %d OpenMP threads)" % threads,
         "frame_s": round(secs, 3),
-        "extrapolated": P > 4,
+        "extrapolated": not full,
         "host_nproc": nproc,
         "affinity_threads": affinity,
         "threads_from": "--cpu-threads" if args.cpu_threads else ("OMP_NUM_THREADS (the pool's CPU share per GPU; "
@@ -246,6 +256,9 @@ def roofline(excl, counted, launches, trace_ms, scene_bytes, spheres, workload, 
     if table:
         roof.update(table)
     iss = load_issue(workload)
+    timed = timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps)
+    if timed:
+        roof["timed"] = timed
     if iss and steps:
         ms_pass = elapsed / steps * 1e3
         v_all, v_tr = iss["per_pass"]["SQ_INSTS_VALU"], iss["trace_per_pass"]["SQ_INSTS_VALU"]
@@ -259,6 +272,42 @@ def roofline(excl, counted, launches, trace_ms, scene_bytes, spheres, workload, 
     return roof
 
 
+
+
+def timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps):
+    """The dominant kernel inside the timed step (up to 20 passes sharing the chip): its time per step is
+    taken as its share of one pass's wave residency (rocprofv3 --pmc SQ_WAVE_CYCLES of the trace launches
+    over every kernel's, profiles/pmc_issue.json) times ms_per_step, so it never exceeds the step; over
+    that time, one pass's algorithmic trace bytes, its measured fabric bytes (profiles/pmc_traffic.json)
+    and its VALU wave-instructions, against the HBM peak and the chip's VALU issue rate."""
+    if not (iss and steps and elapsed > 0 and launches and counted):
+        return None
+    wc_all = iss.get("per_pass", {}).get("SQ_WAVE_CYCLES")
+    wc_tr = iss.get("trace_per_pass", {}).get("SQ_WAVE_CYCLES")
+    if not (wc_all and wc_tr):
+        return None
+    share = wc_tr / wc_all
+    ms_pass = elapsed / steps * 1e3
+    t = share * ms_pass / 1e3                       # s of trace per step
+    alg = compulsory_trace_bytes(counted, scene_bytes, launches, per_xcd=True) / steps
+    out = {"wave_cycle_share": round(share, 4), "ms_per_step": round(share * ms_pass, 4),
+           "step_ms": round(ms_pass, 3),
+           "algorithmic_bytes_per_step": int(alg), "achieved": round(alg / t / 1e9, 1),
+           "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
+    if pmc and pmc.get("trace_bytes_per_launch") and pmc.get("passes_profiled"):
+        meas = pmc["trace_bytes_per_launch"] * pmc["trace_launches"] / pmc["passes_profiled"]
+        out.update({"measured_bytes_per_step": int(meas), "measured_achieved": round(meas / t / 1e9, 1),
+                    "measured_frac": round(meas / t / 1e9 / HBM_PEAK_GBS, 4)})
+    v_tr = iss.get("trace_per_pass", {}).get("SQ_INSTS_VALU")
+    if v_tr:
+        out["valu_frac"] = round(v_tr / t / 1e9 / VALU_PEAK_GWIS, 4)
+    out["def"] = ("trace_kernel within the timed step: its share of one pass's wave residency (SQ_WAVE_CYCLES of "
+                  "the trace launches / every kernel's, PMC run of one pass, profiles/pmc_issue.json: %s) x "
+                  "ms_per_step = its time per step (<= ms_per_step); frac = one pass's algorithmic trace bytes "
+                  "(as achieved_def) / that time / HBM peak; measured_frac = the PMC fabric bytes of the pass's "
+                  "trace launches (profiles/pmc_traffic.json) / that time / HBM peak; valu_frac = the pass's trace "
+                  "VALU wave-instructions / that time / the chip's VALU issue rate" % iss.get("run", ""))
+    return out
 
 
 def per_launch_table(excl, scene_bytes, pmc):

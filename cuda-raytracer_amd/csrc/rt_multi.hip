@@ -37,6 +37,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -201,6 +202,7 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
     if (!run.setup()) return rtamd::fail(RT_E_INVALID, "another device of the render failed");
     if (injected_failure(st.rank)) return rtamd::fail(RT_E_INVALID, "injected failure (RTAMD_FAIL_AFTER_SETUP)");
     using clk = std::chrono::high_resolution_clock;
+    const auto loop0 = clk::now();
     // Overlapped exchange (the default; RTAMD_XCHG_OVERLAP=0: one exchange after each chunk's render):
     // the chunk's passes are enqueued without waiting (rt_renderer_run_async), and the exchange
     // stream takes the slices of every `xr` rounds as soon as this device's passes of those rounds
@@ -258,12 +260,18 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
         MWAIT(g.s);
         st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     }
+    const double loop_ms = std::chrono::duration<double, std::milli>(clk::now() - loop0).count();
     const auto t0 = clk::now();
     // gather the finished slices to the root (in place: the root's own slice is block 0)
     MNCCL(ncclGather(slice, slice, sl, ncclFloat32, 0, comm, g.s));
     if (st.rank == 0) MHIP(hipMemcpyAsync(fb_out, slice, px3 * sizeof(float), hipMemcpyDeviceToHost, g.s));
     MWAIT(g.s);
     st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    if (std::getenv("RTAMD_TIMING"))
+        std::fprintf(stderr, "rt_multi device %d: %d passes rendered and exchanged in %.2f ms (exchange not hidden: %.2f ms, "
+                     "%s), then gather + framebuffer to the host %.2f ms\n", st.rank, (int)st.stats.passes, loop_ms,
+                     st.exchange_ms, overlap ? "overlapped" : "after each chunk",
+                     std::chrono::duration<double, std::milli>(clk::now() - t0).count());
     run.ok = true;
     return RT_OK;
 }

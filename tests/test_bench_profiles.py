@@ -1,6 +1,6 @@
 """The committed PMC summaries that bench.py prices its roofline with (profiles/pmc_traffic.json,
 profiles/pmc_issue.json) are present for the headline workload, come from exactly one profiled pass,
-and give fractions <= 1 at the measured pass time (profiles/r04/final/bench_teapot.json)."""
+and give fractions <= 1 at the measured pass time (the bench line measured with them: profiles/r05/head)."""
 import importlib
 import json
 import os
@@ -19,7 +19,7 @@ def _bench():
 
 
 def _bench_line():
-    with open(os.path.join(REPO, "profiles", "r04", "final", "bench_teapot.json")) as f:
+    with open(os.path.join(REPO, "profiles", "r05", "head", "bench_steps20.json")) as f:
         return json.loads(f.read().strip().splitlines()[-1])
 
 
@@ -47,6 +47,9 @@ def test_bench_line_fractions_at_most_one():
     assert 0 < roof["frac"] <= 1 and 0 < roof["traffic_frac"] <= 1
     assert 0 < roof["l2"]["frac"] <= 1 and 0 < roof["frame"]["frac"] <= 1
     assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
+    t = roof["timed"]                                   # round 5: the trace kernel inside the timed step
+    assert 0 < t["ms_per_step"] <= t["step_ms"] and 0 < t["frac"] <= 1 and 0 < t["measured_frac"] <= 1
+    assert 0 < t["valu_frac"] <= 1
 
 
 def test_roofline_restated_on_exclusive_launches():
@@ -130,3 +133,23 @@ def test_roofline_per_launch_table_recomputes():
     pmc = bench.load_pmc(WORKLOAD)
     assert [r["measured_bytes"] for r in rows] == pmc["trace_bytes_by_launch"]
     assert pmc["run"].startswith("rev ")
+
+
+def test_timed_regime_fits_the_step():
+    """Round 5 (roofline.timed): the trace kernel's time per step is its wave-residency share of a pass times
+    ms_per_step, so it never exceeds the step, and every fraction recomputes from the bytes / instructions
+    per pass over that time."""
+    bench = _bench()
+    counted = {"live_segments": 20 * 79_000_000, "generated_rays": 20 * 41_472_000}
+    scene_bytes = 32 * 252_099 + 48 * 126_050
+    iss = {"per_pass": {"SQ_WAVE_CYCLES": 4.0e9, "SQ_INSTS_VALU": 3.6e9},
+           "trace_per_pass": {"SQ_WAVE_CYCLES": 3.0e9, "SQ_INSTS_VALU": 3.0e9}, "run": "synthetic"}
+    pmc = {"trace_bytes_per_launch": 250e6, "trace_launches": 16, "passes_profiled": 1}
+    t = bench.timed_regime(iss, pmc, counted, 20 * 16, scene_bytes, 0.128, 20)
+    assert t["wave_cycle_share"] == 0.75 and t["ms_per_step"] <= t["step_ms"]
+    secs = 0.75 * 0.128 / 20
+    alg = bench.compulsory_trace_bytes(counted, scene_bytes, 20 * 16, per_xcd=True) / 20
+    assert abs(t["frac"] - alg / secs / 1e9 / bench.HBM_PEAK_GBS) < 1e-4
+    assert abs(t["measured_frac"] - 16 * 250e6 / secs / 1e9 / bench.HBM_PEAK_GBS) < 1e-4
+    assert abs(t["valu_frac"] - 3.0e9 / secs / 1e9 / bench.VALU_PEAK_GWIS) < 1e-4
+    assert bench.timed_regime({"per_pass": {}, "trace_per_pass": {}}, pmc, counted, 320, scene_bytes, 0.128, 20) is None

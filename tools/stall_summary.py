@@ -45,7 +45,8 @@ if "--json" in opts:
     passes = sum(1 for (k, i) in disp if k.startswith("fill_live_kernel")) or 1
     tot, trace = collections.Counter(), collections.Counter()
     for (k, i), d in disp.items():
-        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS"):
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS",
+                  "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"):
             tot[c] += d.get(c, 0)
             if k.startswith("trace_kernel"):
                 trace[c] += d.get(c, 0)
@@ -61,7 +62,9 @@ if "--json" in opts:
         "trace_per_pass": {c: v / passes for c, v in trace.items()},
         "run": opts.get("--run", ""),
         "source": "tools/pmc.sh %s tools/pmc_groups/stall.txt + tools/stall_summary.py" % " ".join(argv),
-        "note": "wave-instructions summed over every dispatch of the profiled pass(es), chip-wide",
+        "note": "wave-instructions summed over every dispatch of the profiled pass(es), chip-wide; "
+                "SQ_WAVE_CYCLES (quad-cycles of resident waves) summed the same way, so trace / all is the trace "
+                "kernel's share of the pass's wave residency (bench.py roofline.timed)",
     }
     with open(path, "w") as f:
         json.dump(doc, f, indent=1, sort_keys=True)
