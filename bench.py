@@ -35,8 +35,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 # on lamp).  With torch.distributed (RCCL) in the process its streams need queues too (16 passes
 # and 16 queues cost the 1-GPU --dist run 11 %).  Set before HIP initialises.
 _DIST = int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dist" in sys.argv
-_QUEUES = 28 if _DIST else 24
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _QUEUES:
+_QUEUES = int(os.environ.get("RTAMD_HW_QUEUES", "0") or 0) or (28 if _DIST else 24)   # RTAMD_HW_QUEUES: sweeps only
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _QUEUES or "RTAMD_HW_QUEUES" in os.environ:
     os.environ["GPU_MAX_HW_QUEUES"] = str(_QUEUES)
 # Next to RCCL, 16 passes in flight beat 20 (1-GPU --dist: 7.63 vs 7.76 ms/pass for a frame, 8.10
 # vs 9.0-12.7 for a 13-pass share); alone, 20 are faster.
@@ -44,6 +44,10 @@ if _DIST:
     os.environ.setdefault("RTAMD_INFLIGHT", "16")
 sys.path.insert(0, os.path.join(REPO, "cuda-raytracer_amd"))
 sys.path.insert(0, os.path.join(REPO, "tools"))
+if os.environ.get("RTAMD_TORCH_FIRST") == "1" and __name__ == "__main__":
+    # diagnostic: torch (and its bundled HIP runtime) loaded first, as in the torch.distributed path
+    import torch
+    torch.cuda.set_device(0)
 
 import numpy as np  # noqa: E402
 
@@ -543,6 +547,10 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
             frame = rtamd_dist.TileShardedFrame(dist, torch, W, H, backend.device,
                                                 lambda out: ren.copy_framebuffer(out.data_ptr()), rows=TILE_ROWS)
         else:
+            # the owners add the pass slices themselves: the renderer's own framebuffer add chain (each
+            # pass's add waits for the previous pass's, across streams) is turned off
+            if hasattr(ren, "set_accumulate"):
+                ren.set_accumulate(False)
             async_render = backend.async_render(ren, accumulate_stats) if hasattr(backend, "async_render") else None
             frame = rtamd_dist.PassShardedFrame(dist, torch, px3, P, backend.device, render_passes,
                                                 async_render=async_render)

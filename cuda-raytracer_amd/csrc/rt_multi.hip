@@ -191,6 +191,9 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
             rt_renderer_destroy(r);
         }
     } g{ren, run};
+    // the owners add the pass slices themselves: no framebuffer add chain across the pass streams
+    rc = rt_renderer_set_accumulate(ren, 0);
+    if (rc) return rc;
     float *&buf = g.bufs[0], *&recv = g.bufs[1], *&slice = g.bufs[2];
     MHIP(hipMalloc(reinterpret_cast<void **>(&buf), (size_t)chunk * pitch * sizeof(float)));
     MHIP(hipMalloc(reinterpret_cast<void **>(&recv), (size_t)chunk * pitch * sizeof(float)));

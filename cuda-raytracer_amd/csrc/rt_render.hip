@@ -584,7 +584,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
         // The child refs are loaded by node lanes only: a leaf lane's step is 3 L1 accesses instead
         // of 4, and the gather rate of L1 accesses bounds the heavy bounces (tools/experiments/
         // gather_bench.hip).  Round 4, A/B on one box: teapot 20 steps 6.89 -> 6.81, full frame
-        // 6.71 -> 6.61, lamp 12.94 -> 12.70 ms/pass (profiles/r04/ab_kids.txt).  Loading only e2.z
+        // 6.71 -> 6.61, lamp 12.94 -> 12.70 ms/pass (docs/history/profiles/r04/ab_kids.txt).  Loading only e2.z
         // for leaf lanes as well (a divergent one-dword load) was slower: 7.74.
         const float4 a = rec[0], b = rec[1], c = rec[2];
         uint2 kids = make_uint2(0, 0);
@@ -2069,6 +2069,12 @@ struct rt_renderer {
     // the async calls leave it alone, and a run that finishes cleanly clears it.
     bool failed = false;
     bool enqueued = false;            // run_impl got past validation (set per call)
+    // Framebuffer accumulation (rt_renderer_set_accumulate).  Each pass's add waits for the previous
+    // pass's add on another stream; when streams outnumber the hardware queues they share in-order
+    // queues, and such a wait holds up every pass queued behind it there (torch's HIP runtime on the
+    // torch.distributed path: 20 passes in flight ran at 11.0 instead of 6.5 ms/pass).
+    // The multi-GPU drivers add the pass sums themselves and turn it off, so no pass stream waits.
+    bool accumulate = true;
     int run(int pass_begin, int count, int stride, float *pass_sums, rt_stats *st, size_t pitch = 0) {
         if (run_pending) return rtamd::fail(RT_E_INVALID, "rt_renderer_run: an async run is not finished");
         int rc = run_impl(pass_begin, count, stride, pass_sums, st, pitch, false);
@@ -2124,6 +2130,8 @@ struct rt_renderer {
         if (tsort() && !xfn)
             return rtamd::fail(RT_E_INVALID, "pixel tiles with sort on need the per-bounce exchange "
                                              "(rt_renderer_set_exchange)");
+        if (!accumulate && !pass_sums)
+            return rtamd::fail(RT_E_INVALID, "framebuffer accumulation is off: the pass sums buffer is required");
         enqueued = true;
         const int inflight = std::min(nctx, std::max(1, P));
         {   // the trace grid of this run, for the passes it actually keeps in flight
@@ -2145,6 +2153,8 @@ struct rt_renderer {
         const int64_t px3 = (int64_t)width * height * 3;
         hipEvent_t prev_fb = nullptr;
         auto add_pass = [&](PassCtx &c, int p, float *sums) -> int {
+            generated += (int64_t)std::min(spp - 20 * p, 20) * tile_pixels();
+            if (!accumulate) return RT_OK;      // the caller adds the pass sums (rt_renderer_set_accumulate)
             if (prev_fb) HIPCHK(hipStreamWaitEvent(c.stream, prev_fb, 0));
             if ((reinterpret_cast<uintptr_t>(sums) & 15) == 0)
                 hipLaunchKernelGGL(add4_kernel, dim3(blocks_for(std::max<int64_t>(px3 / 4, 4))), dim3(kBlock), 0, c.stream,
@@ -2154,7 +2164,6 @@ struct rt_renderer {
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c.fb_done, c.stream));
             prev_fb = c.fb_done;
-            generated += (int64_t)std::min(spp - 20 * p, 20) * tile_pixels();
             return RT_OK;
         };
         auto sums_of = [&](PassCtx &c, int k) {
@@ -2663,6 +2672,13 @@ int rtamd_renderer_set_poll(rt_renderer *r, int (*fn)(void *), void *user) {
     if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
     r->xpoll = fn;
     r->xpoll_user = user;
+    return RT_OK;
+}
+
+int rt_renderer_set_accumulate(rt_renderer *r, int32_t enable) {
+    if (!r) return rtamd::fail(RT_E_INVALID, "null renderer");
+    if (int rc = r->busy("rt_renderer_set_accumulate")) return rc;
+    r->accumulate = enable != 0;
     return RT_OK;
 }
 

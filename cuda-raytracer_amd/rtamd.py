@@ -361,6 +361,13 @@ class Renderer:
     def set_counters(self, on):
         _check(lib().rt_renderer_set_counters(self.h, int(on)))
 
+    def set_accumulate(self, on):
+        """Framebuffer accumulation (rt_renderer_set_accumulate; default on).  Off: runs need d_pass_sums
+        and only write them (the multi-GPU drivers add the pass slices themselves)."""
+        f = lib().rt_renderer_set_accumulate
+        f.argtypes = [P, I32]
+        _check(f(self.h, int(on)))
+
     def launch_profile(self, cap=256):
         """Per trace launch of the last event-timed run's first pass: [(span ms, live rays), ...]
         (rt_renderer_launch_profile)."""

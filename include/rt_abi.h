@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 enum {
     RT_OK = 0,
@@ -218,6 +218,11 @@ int rt_renderer_set_exchange(rt_renderer *r, rt_exchange_fn fn, void *user, int3
 int rt_rccl_unique_id(uint8_t *id_out);
 int rt_renderer_set_exchange_rccl(rt_renderer *r, const uint8_t *id, int32_t nranks, int32_t rank);
 int rt_renderer_set_counters(rt_renderer *r, int32_t enable);
+/* Framebuffer accumulation (default on).  Off, a run must be given d_pass_sums and only writes them:
+ * no pass is added into the renderer's framebuffer, so no pass's stream waits for another's (the
+ * in-order add chain is what the multi-GPU drivers, which add the pass slices themselves, turn off).
+ * No reference counterpart. */
+int rt_renderer_set_accumulate(rt_renderer *r, int32_t enable);
 /* Per-bounce HIP events behind rt_stats.process_ms / sort_ms (default on).  Off, those stay 0 and
  * a pass's stream carries no marker packets between its kernels (~2 % faster frames). */
 int rt_renderer_set_event_timing(rt_renderer *r, int32_t enable);

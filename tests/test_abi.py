@@ -43,7 +43,7 @@ def test_struct_layouts():
     assert C.sizeof(R.RtOpts) == 56   # + tile_count/index/rows, device_count, device_ids*, shard_tiles
     assert C.sizeof(R.RtLoadOpts) == 48
     assert C.sizeof(R.RtStats) == 11 * 8 + 8 + 5 * 8 + 8 + 8
-    assert R.lib().rt_abi_version() == 5
+    assert R.lib().rt_abi_version() == 6
 
 
 def test_default_options():

@@ -72,8 +72,11 @@ def test_roofline_restated_on_exclusive_launches():
     assert roof["logical_per_step"]["achieved"] > 0
 
 
+FINAL = os.path.join(REPO, "docs", "history", "profiles", "r04", "final")   # the last closing measurement
+
+
 def _final_lines():
-    d = os.path.join(REPO, "profiles", "r04", "final")
+    d = FINAL
     out = {}
     for f in sorted(os.listdir(d)):
         if f.startswith("bench_") and f.endswith(".json"):
@@ -83,7 +86,7 @@ def _final_lines():
 
 
 def test_closing_lines_every_config_bit_exact():
-    """Round 4's closing measurement (profiles/r04/final): a line per BASELINE config, each with its pass-0
+    """The closing measurement (FINAL): a line per BASELINE config, each with its pass-0
     framebuffer hash equal to the oracle's and its fractions at most one."""
     lines = _final_lines()
     for name in ("bench_cornell.json", "bench_cornell_plus.json", "bench_spheres.json", "bench_teapot.json",
@@ -112,7 +115,7 @@ def test_closing_exclusive_launch_agrees_with_the_profiler():
 def test_results_table_from_committed_files():
     import subprocess
     out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "results_table.py"),
-                          os.path.join(REPO, "profiles", "r04", "final")], capture_output=True, text=True, check=True).stdout
+                          FINAL], capture_output=True, text=True, check=True).stdout
     rows = [r for r in out.splitlines() if r.startswith("| ") and " | 1 | " in r]
     assert len(rows) == 7, out                      # 5 configs, teapot and lamp in both sort modes
     assert all("| True |" in r for r in rows)

@@ -84,3 +84,36 @@ def test_async_run_misuse_is_refused(torch_gpu):
         ren.run(0, 2)                                       # the renderer is usable again
     finally:
         ren.close()
+
+
+def test_accumulate_off_writes_pass_sums_only(torch_gpu):
+    """rt_renderer_set_accumulate(0) (round 5, the multi-GPU drivers): the run writes each pass's sums, bit-exact
+    against the oracle's, and adds nothing into the renderer's framebuffer; without a pass sums buffer such a
+    run is refused."""
+    torch = torch_gpu
+    path = "%s/teapot.scene" % R.ASSETS
+    osc, psc = O.OracleScene(path, image=IMAGE), R.Scene(path, image=IMAGE)
+    ref_sums = osc.pass_sums(sort=True, pass_begin=0, pass_count=psc.passes)
+    ren = R.Renderer(psc, sort=True)
+    try:
+        ren.set_accumulate(False)
+        with pytest.raises(R.RtError):
+            ren.run(0, 1)                                   # nowhere to put the sums
+        out = torch.zeros((psc.passes, psc.pixels * 3), dtype=torch.float32, device="cuda")
+        ren.run(0, psc.passes, 1, out.data_ptr())
+        for k in range(psc.passes):
+            assert np.array_equal(out[k].cpu().numpy(), ref_sums[k]), "pass %d" % k
+        out.zero_()
+        ren.run_async(0, psc.passes, 1, out.data_ptr())
+        with pytest.raises(R.RtError):
+            ren.set_accumulate(True)                        # refused while the run is pending
+        ren.finish()
+        for k in range(psc.passes):
+            assert np.array_equal(out[k].cpu().numpy(), ref_sums[k]), "async pass %d" % k
+        assert not ren.framebuffer().any()                  # nothing was accumulated
+        ren.set_accumulate(True)
+        ren.run(0, psc.passes)
+        ref_fb, _ = osc.render(sort=True)
+        assert np.array_equal(ren.framebuffer(), ref_fb)
+    finally:
+        ren.close()

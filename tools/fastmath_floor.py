@@ -13,7 +13,7 @@ the passes): the Monte-Carlo noise floor.  Any implementation that differs from 
 by fast-math rounding differs from it by about the first figure; no implementation can reach a
 per-pixel tolerance below it.
 
-    python tools/fastmath_floor.py [--out profiles/r04/fastmath_floor.json]
+    python tools/fastmath_floor.py [--out profiles/r05/fastmath_floor.json]
 """
 import argparse
 import json
@@ -83,7 +83,7 @@ def main():
         render(a[0], *[int(x) for x in a[1:7]], a[7], int(a[8]))
         return
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r04", "fastmath_floor.json"))
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r05", "fastmath_floor.json"))
     ap.add_argument("--threads", type=int, default=8)
     args = ap.parse_args()
     import make_envmap

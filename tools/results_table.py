@@ -2,13 +2,13 @@
 BASELINE config x GPUs.  1-GPU cells come from profiles/<round>/bench_*.json and profiles/pmc_traffic.json;
 N > 1 has no hardware measurement (the driver's SCALE run is the only one), so those rows say so.
 
-    python tools/results_table.py [profiles/r04/final]"""
+    python tools/results_table.py [profiles/r05/final]"""
 import json
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-D = os.path.abspath(sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r04", "final"))
+D = os.path.abspath(sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r05", "final"))
 ROWS = [("1 cornell 256² × 64 × 4", "bench_cornell.json"),
         ("2 cornell_plus 512² × 256 × 8", "bench_cornell_plus.json"),
         ("3 spheres 1024² × 1024 × 8", "bench_spheres.json"),
