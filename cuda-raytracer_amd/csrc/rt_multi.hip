@@ -51,6 +51,8 @@ int fail(int code, const std::string &msg);
 extern "C" int rtamd_renderer_set_poll(rt_renderer *r, int (*fn)(void *), void *user);   // rt_render.hip
 extern "C" int rtamd_renderer_run_pitched(rt_renderer *r, int pass_begin, int count, int stride,
                                           float *d_pass_sums, size_t pitch, rt_stats *stats);   // rt_render.hip
+extern "C" int rtamd_renderer_create_inflight(const rt_scene *scene, const rt_opts *opts, rt_renderer **out,
+                                              int inflight);                                 // rt_render.hip
 extern "C" int rtamd_renderer_run_async_pitched(rt_renderer *r, int pass_begin, int count, int stride,
                                                 float *d_pass_sums, size_t pitch);             // rt_render.hip
 
@@ -70,6 +72,8 @@ __global__ __launch_bounds__(256) void add_slices_kernel(float *__restrict__ sli
 }
 
 const char *nccl_str(ncclResult_t r) { return ncclGetErrorString(r); }
+
+constexpr int kInflightNextToRccl = 16;   // passes in flight of a device's renderer (run_device)
 
 struct DevState {
     int device = 0, rank = 0;
@@ -176,7 +180,11 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
     o.pass_stride = 1;
     o.tile_count = 0;
     rt_renderer *ren = nullptr;
-    int rc = rt_renderer_create(scene, &o, &ren);
+    // Passes in flight next to RCCL: each pass's stream needs a hardware queue of its own -- two
+    // streams on one in-order queue run their passes one after the other -- and the communicator's
+    // streams take queues too (one-GPU probe, 26 passes: 7.07 ms/pass at 16 in flight, 7.50 at 20;
+    // DESIGN §7).  bench.py's torch.distributed path uses the same 16.
+    int rc = rtamd_renderer_create_inflight(scene, &o, &ren, kInflightNextToRccl);
     if (rc) return rc;
     struct Guard {
         rt_renderer *r;

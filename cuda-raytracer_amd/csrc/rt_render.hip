@@ -1443,6 +1443,7 @@ struct rt_renderer {
                                                     : kStaggerUs;
     PassCtx ctx[kInflight];
     int pass_hint = 0;                // rt_render: the passes this renderer will ever run (0: any)
+    int inflight_limit = 0;           // a cap on passes in flight set by the creator (rt_multi next to RCCL)
     int trace_blocks = 0;             // persistent trace_kernel grid of the current run
     int trace_blocks_max = 0;         // all resident trace workgroups (the overflow stacks are sized for it)
     int nctx = 1;                     // pass contexts allocated (passes in flight)
@@ -1624,6 +1625,7 @@ struct rt_renderer {
         // RTAMD_INFLIGHT caps the passes in flight below kInflight (bench.py: 16 next to RCCL, where
         // 20 contexts ran a 13-pass share at 12.7 instead of 8.1 ms/pass)
         size_t cap = kInflight;
+        if (inflight_limit > 0) cap = std::min<size_t>(cap, (size_t)inflight_limit);
         if (const char *e = std::getenv("RTAMD_INFLIGHT")) cap = std::min<size_t>(cap, (size_t)std::max(1, std::atoi(e)));
         inflight_cap = (int)cap;
         if (pass_hint > 0) cap = std::min<size_t>(cap, (size_t)pass_hint);   // a one-shot render of fewer passes
@@ -2497,7 +2499,8 @@ int rt_device_warmup(int32_t device) {
 }
 
 namespace {
-int create_renderer(const rt_scene *scene, const rt_opts *opts, rt_renderer **out, int pass_hint) {
+int create_renderer(const rt_scene *scene, const rt_opts *opts, rt_renderer **out, int pass_hint,
+                    int inflight_limit = 0) {
     if (!out) return rtamd::fail(RT_E_INVALID, "null output");
     *out = nullptr;
     int rc = check_scene(scene);
@@ -2507,6 +2510,7 @@ int create_renderer(const rt_scene *scene, const rt_opts *opts, rt_renderer **ou
     if (rt_device_count() <= o.device || o.device < 0) return rtamd::fail(RT_E_NODEVICE, "no such HIP device");
     auto *r = new rt_renderer();
     r->pass_hint = pass_hint;
+    r->inflight_limit = inflight_limit;
     rc = r->init(scene, &o);
     if (rc) { delete r; return rc; }
     *out = r;
@@ -2516,6 +2520,11 @@ int create_renderer(const rt_scene *scene, const rt_opts *opts, rt_renderer **ou
 
 int rt_renderer_create(const rt_scene *scene, const rt_opts *opts, rt_renderer **out) {
     return create_renderer(scene, opts, out, 0);
+}
+
+// rt_multi.hip: a renderer with at most `inflight` passes in flight (RTAMD_INFLIGHT may lower it further)
+int rtamd_renderer_create_inflight(const rt_scene *scene, const rt_opts *opts, rt_renderer **out, int inflight) {
+    return create_renderer(scene, opts, out, 0, inflight);
 }
 
 int rtamd_renderer_run_pitched(rt_renderer *r, int pass_begin, int count, int stride, float *d_pass_sums,
