@@ -1,6 +1,6 @@
 """The committed PMC summaries that bench.py prices its roofline with (profiles/pmc_traffic.json,
 profiles/pmc_issue.json) are present for the headline workload, come from exactly one profiled pass,
-and give fractions <= 1 at the measured pass time (the bench line measured with them: profiles/r05/head)."""
+and give fractions <= 1 at the measured pass time (the closing bench lines measured with them: profiles/r05/final)."""
 import importlib
 import json
 import os
@@ -8,6 +8,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKLOAD = "teapot.scene 1920x1080 2048spp 16 bounces sort=on"
+FINAL = os.path.join(REPO, "profiles", "r05", "final")   # the closing measurement of this round
 
 
 def _bench():
@@ -19,7 +20,7 @@ def _bench():
 
 
 def _bench_line():
-    with open(os.path.join(REPO, "profiles", "r05", "head", "bench_steps20.json")) as f:
+    with open(os.path.join(FINAL, "bench_teapot.json")) as f:
         return json.loads(f.read().strip().splitlines()[-1])
 
 
@@ -72,7 +73,6 @@ def test_roofline_restated_on_exclusive_launches():
     assert roof["logical_per_step"]["achieved"] > 0
 
 
-FINAL = os.path.join(REPO, "docs", "history", "profiles", "r04", "final")   # the last closing measurement
 
 
 def _final_lines():
