@@ -83,6 +83,69 @@ struct DevState {
     double exchange_ms = 0;
 };
 
+// Test transport (RTAMD_MULTI_LOOPBACK=1): the "devices" are host threads on ONE GPU (device_ids may repeat),
+// and run_device's two collectives become device-to-device copies between the threads' buffers, ordered through
+// events the threads swap at host barriers.  It exists so that the multi-device schedule -- pass dealing, the
+// stale rows of rounds a device has no pass in, the owners' ordered adds, the gather -- runs at N > 1 on a
+// one-GPU box (RCCL refuses two ranks on one GPU); the product path is RCCL.  No abort handling: tests only.
+struct Loopback {
+    int world = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    std::vector<hipEvent_t> ev_in, ev_out;    // per rank, re-recorded at every collective
+    std::vector<float *> send, recv;          // per rank: the current collective's buffers
+    void barrier() {
+        std::unique_lock<std::mutex> l(m);
+        const uint64_t g = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(l, [&] { return gen != g; });
+        }
+    }
+    // entry: every rank's stream waits for every rank's work so far; exit: for every rank's copies
+    int fence(std::vector<hipEvent_t> &ev, int rank, hipStream_t s) {
+        if (hipEventRecord(ev[rank], s) != hipSuccess) return RT_E_HIP;
+        barrier();
+        for (int p = 0; p < world; p++)
+            if (p != rank && hipStreamWaitEvent(s, ev[p], 0) != hipSuccess) return RT_E_HIP;
+        return RT_OK;
+    }
+    // ncclAllToAll of rows j0..j1 (sl floats per destination, rows `pitch` floats apart): recv[j][src] =
+    // src's buf[j][rank]
+    int alltoall(int rank, float *buf, float *rv, int j0, int j1, size_t pitch, size_t sl, hipStream_t s) {
+        send[rank] = buf;
+        recv[rank] = rv;
+        if (int rc = fence(ev_in, rank, s)) return rc;
+        for (int j = j0; j < j1; j++)
+            for (int src = 0; src < world; src++)
+                if (hipMemcpyAsync(rv + (size_t)j * pitch + (size_t)src * sl, send[src] + (size_t)j * pitch + (size_t)rank * sl,
+                                   sl * sizeof(float), hipMemcpyDeviceToDevice, s) != hipSuccess)
+                    return RT_E_HIP;
+        return fence(ev_out, rank, s);
+    }
+    // ncclGather of every rank's sl-float slice into root's buffer, block src at src * sl (root's own in place)
+    int gather(int rank, float *slice, size_t sl, hipStream_t s) {
+        send[rank] = slice;
+        if (int rc = fence(ev_in, rank, s)) return rc;
+        if (rank == 0)
+            for (int src = 1; src < world; src++)
+                if (hipMemcpyAsync(slice + (size_t)src * sl, send[src], sl * sizeof(float), hipMemcpyDeviceToDevice, s) !=
+                    hipSuccess)
+                    return RT_E_HIP;
+        return fence(ev_out, rank, s);
+    }
+};
+
+bool loopback_requested() {
+    const char *e = std::getenv("RTAMD_MULTI_LOOPBACK");
+    return e && std::atoi(e) != 0;
+}
+
 void add_stats(DevState &st, const rt_stats &s) {
     st.stats.live_segments += s.live_segments;
     st.stats.generated_rays += s.generated_rays;
@@ -160,7 +223,7 @@ int wait_stream(hipStream_t s, Link &ln) {
 
 // Device `st.rank`'s share of the frame: render, exchange, add; the root also gathers.
 int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, DevState &st, float *fb_out,
-               Sync &sy) {
+               Sync &sy, Loopback *lb) {
     RunGuard run{sy, ln};
     ncclComm_t comm = ln.comm;
     MHIP(hipSetDevice(st.device));
@@ -250,10 +313,15 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
                     rc = rt_renderer_wait_pass(ren, j, g.s);
                     if (rc) return rc;
                 }
-            MNCCL(ncclGroupStart());
-            for (int j = j0; j < j1; j++)
-                MNCCL(ncclAllToAll(buf + (size_t)j * pitch, recv + (size_t)j * pitch, sl, ncclFloat32, comm, g.s));
-            MNCCL(ncclGroupEnd());
+            if (lb) {
+                if (int rc2 = lb->alltoall(st.rank, buf, recv, j0, j1, pitch, sl, g.s))
+                    return rtamd::fail(rc2, "loopback exchange failed");
+            } else {
+                MNCCL(ncclGroupStart());
+                for (int j = j0; j < j1; j++)
+                    MNCCL(ncclAllToAll(buf + (size_t)j * pitch, recv + (size_t)j * pitch, sl, ncclFloat32, comm, g.s));
+                MNCCL(ncclGroupEnd());
+            }
             hipLaunchKernelGGL(add_slices_kernel, dim3((unsigned)((sl + 255) / 256)), dim3(256), 0, g.s, slice,
                                recv + (size_t)j0 * pitch, sl, world, j1 - j0, k0 + j0, P);
             MHIP(hipGetLastError());
@@ -274,7 +342,11 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
     const double loop_ms = std::chrono::duration<double, std::milli>(clk::now() - loop0).count();
     const auto t0 = clk::now();
     // gather the finished slices to the root (in place: the root's own slice is block 0)
-    MNCCL(ncclGather(slice, slice, sl, ncclFloat32, 0, comm, g.s));
+    if (lb) {
+        if (int rc2 = lb->gather(st.rank, slice, sl, g.s)) return rtamd::fail(rc2, "loopback gather failed");
+    } else {
+        MNCCL(ncclGather(slice, slice, sl, ncclFloat32, 0, comm, g.s));
+    }
     if (st.rank == 0) MHIP(hipMemcpyAsync(fb_out, slice, px3 * sizeof(float), hipMemcpyDeviceToHost, g.s));
     MWAIT(g.s);
     st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
@@ -365,11 +437,14 @@ int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out
     const int world = opts->device_count;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    const bool loopback = loopback_requested();
+    if (loopback && opts->shard_tiles)
+        return rtamd::fail(RT_E_INVALID, "RTAMD_MULTI_LOOPBACK covers pass sharding only (not shard_tiles)");
     std::vector<int> devs(world);
     for (int k = 0; k < world; k++) {
-        devs[k] = opts->device_ids ? opts->device_ids[k] : k;
+        devs[k] = opts->device_ids ? opts->device_ids[k] : (loopback ? 0 : k);
         if (devs[k] < 0 || devs[k] >= ndev) return rtamd::fail(RT_E_NODEVICE, "device_ids: no such HIP device");
-        for (int j = 0; j < k; j++)
+        for (int j = 0; j < k && !loopback; j++)
             if (devs[j] == devs[k]) return rtamd::fail(RT_E_INVALID, "device_ids: a device is listed twice");
     }
     if (opts->tile_count > 1) return rtamd::fail(RT_E_INVALID, "device_count and tile_count are exclusive "
@@ -377,8 +452,27 @@ int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out
     if (opts->pass_begin != 0 || (opts->pass_count != -1 && opts->pass_count != (scene->ray_count + 19) / 20) ||
         opts->pass_stride > 1)
         return rtamd::fail(RT_E_INVALID, "multi-device rt_render renders the whole frame (pass_begin 0, all passes)");
-    std::vector<ncclComm_t> comms(world);
-    {
+    std::vector<ncclComm_t> comms(world, nullptr);
+    Loopback lb;
+    struct LbEvents {
+        Loopback &lb;
+        ~LbEvents() {
+            for (auto e : lb.ev_in) if (e) (void)hipEventDestroy(e);
+            for (auto e : lb.ev_out) if (e) (void)hipEventDestroy(e);
+        }
+    } lb_events{lb};
+    if (loopback) {
+        lb.world = world;
+        lb.send.assign(world, nullptr);
+        lb.recv.assign(world, nullptr);
+        lb.ev_in.assign(world, nullptr);
+        lb.ev_out.assign(world, nullptr);
+        for (int k = 0; k < world; k++)
+            if (hipSetDevice(devs[k]) != hipSuccess ||
+                hipEventCreateWithFlags(&lb.ev_in[k], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&lb.ev_out[k], hipEventDisableTiming) != hipSuccess)
+                return rtamd::fail(RT_E_HIP, "loopback: hipEventCreate failed");
+    } else {
         const ncclResult_t r = ncclCommInitAll(comms.data(), world, devs.data());
         if (r != ncclSuccess) return rtamd::fail(RT_E_HIP, std::string("Error ncclCommInitAll ") + nccl_str(r));
     }
@@ -396,13 +490,14 @@ int rtamd_render_multi(const rt_scene *scene, const rt_opts *opts, float *fb_out
         st[k].rank = k;
         th.emplace_back([&, k]() {
             st[k].rc = opts->shard_tiles ? run_device_tiles(scene, opts, links[k], world, st[k], fb_out, sy)
-                                         : run_device(scene, opts, links[k], world, st[k], fb_out, sy);
+                                         : run_device(scene, opts, links[k], world, st[k], fb_out, sy,
+                                                      loopback ? &lb : nullptr);
             if (st[k].rc) st[k].err = rt_last_error();
         });
     }
     for (auto &t : th) t.join();
     for (auto &l : links)
-        if (!l.aborted) (void)ncclCommDestroy(l.comm);   // ncclCommAbort already freed the others
+        if (!l.aborted && l.comm) (void)ncclCommDestroy(l.comm);   // ncclCommAbort already freed the others
     // report the device that failed first-hand, not a peer that returned because of it
     for (auto &s : st)
         if (s.rc && s.err.find("another device") == std::string::npos) return rtamd::fail(s.rc, s.err);

@@ -187,6 +187,31 @@ def test_multi_device_rccl_bitexact(gpu, monkeypatch, scene, image, sort, xchg):
     assert gst["exchange_ms"] > 0
 
 
+@pytest.mark.parametrize("world,scene,image,sort,xchg", [
+    (2, "teapot", (64, 36, 100, 16), True, "overlap"),       # 5 passes: device 1 has no pass in the last round
+    (3, "cornell_plus", (40, 32, 350, 5), True, "overlap1"),  # 18 passes, 6 rounds
+    (5, "cornell", (33, 17, 190, 4), False, "sync"),          # 10 passes, odd size: padded slices
+    (2, "cornell", (24, 16, 700, 3), True, "overlap"),        # 35 passes = 18 rounds: two chunks of rounds
+])
+def test_multi_device_loopback_bitexact(gpu, monkeypatch, world, scene, image, sort, xchg):
+    """The in-library multi-device render at N > 1 on the box's one GPU (round 5): RTAMD_MULTI_LOOPBACK=1 runs
+    rt_multi.hip's device threads on the same GPU with its two collectives as device-to-device copies (RCCL refuses
+    two ranks on one GPU), so the pass dealing, the stale rows of rounds a device has no pass in, the overlapped
+    exchange, the owners' ordered adds and the gather all run at N = 2 / 3 / 5: bit-exact against the oracle."""
+    monkeypatch.setenv("RTAMD_MULTI_LOOPBACK", "1")
+    if xchg == "sync":
+        monkeypatch.setenv("RTAMD_XCHG_OVERLAP", "0")
+    elif xchg == "overlap1":
+        monkeypatch.setenv("RTAMD_XCHG_ROUNDS", "1")
+    osc, psc = _pair(scene, image)
+    ofb, ost = osc.render(sort=sort)
+    gfb, gst = R.render(psc, sort=sort, devices=[0] * world)
+    assert np.array_equal(gfb, ofb), _diff(gfb, ofb)
+    assert gst["live_segments"] == ost["live_segments"] and gst["passes"] == psc.passes
+    with pytest.raises(R.RtError, match="pass sharding only"):
+        R.render(psc, sort=sort, devices=[0] * world, shard_tiles=True)
+
+
 def test_multi_device_rejects_bad_device_lists(gpu):
     _, psc = _pair("cornell", (16, 16, 20, 2))
     with pytest.raises(R.RtError, match="twice"):
