@@ -121,6 +121,7 @@ constexpr int kTraceOccPct = RT_TRACE_OCC;
 constexpr int kQueues = RT_QUEUES;   // trace queue shards (one per XCD group of workgroups)
 constexpr int kQueueStride = 64;     // words between shards (256 B: one shard per cache line)
 constexpr uint32_t kDead = 64;        // bucket of a terminated ray (key 0xFFFFFFFF)
+constexpr uint32_t kAccFlag = 0x80000000u;   // in a ray id (rid): acc[ray] holds the ray's radiance so far
 // Per-launch span words (rt_renderer_set_event_timing): 8 start slots then 8 end slots, one per XCD
 // (workgroup i runs on XCD i % 8), each written by one atomic per workgroup -- one word for a whole
 // 8192-wave launch serialised its waves' atomics and lengthened the span it measured (round 3:
@@ -173,7 +174,7 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 // generate_initial_rays (scene.cu:78-105, raytracing.cu:76-81), evaluated where a bounce-0 ray
 // is needed (trace and shade of bounce 0) instead of being written out and read back.  Ray i
 // of a pass is slot i at bounce 0.  Ray state afterwards: geo[2 i .. 2 i + 1] = {o.xyz, d.x},
-// {d.yz, T.xy} (what traversal reads) and tc[i] = {T.z, C.xyz} (what accumulation reads).
+// {d.yz, T.xy} (what traversal reads) and tz[i] = T.z; the radiance goes to acc[ray id] (shade_kernel).
 // n / d for n < 2^31 as a multiply-high and a shift (Granlund-Montgomery: m = ceil(2^(31+l)/d),
 // l = ceil(log2 d)); l = 0 means d = 1.
 struct FastDiv {
@@ -639,9 +640,11 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 // emission + scatter.  Returns the new state; `ray` = the ray id (acc index), kind = 0 miss,
 // 1 triangle hit, 2 sphere hit.
 struct Shaded {
-    V3 no, nd, T, C;
+    V3 no, nd, T;
+    V3 C;                             // this bounce's radiance term as 0 + term (emission or sky times T)
     uint32_t ray;
     int kind;
+    bool acc_holds;                   // acc[ray] holds the radiance of the earlier bounces
 };
 // INLINE (scenes without triangles): the closest hit is the sphere loop (scene.cu:338-372),
 // computed here instead of read from the trace kernel's output.
@@ -651,11 +654,13 @@ struct Shaded {
 struct ShadeIn {
     float2 h;
     uint32_t ray, seed;
-    float4 r0, r1, r2;
+    bool acc_holds;                   // acc[ray] holds the ray's radiance so far (kAccFlag in its rid)
+    float4 r0, r1;
+    float tz;
 };
 template <bool SORTED, int FIRST, bool INLINE>
 __device__ __forceinline__ ShadeIn shade_in(const PassArgs &pa, int slot, const float4 *__restrict__ geo,
-                                            const float4 *__restrict__ tc, const uint32_t *__restrict__ rid,
+                                            const float *__restrict__ tz, const uint32_t *__restrict__ rid,
                                             const float2 *__restrict__ hits, const uint32_t *__restrict__ seed_of) {
     ShadeIn in{};
     // The seed follows the reference's slot (raytracing.cu:89): the position with sort on;
@@ -663,15 +668,17 @@ __device__ __forceinline__ ShadeIn shade_in(const PassArgs &pa, int slot, const 
     // reference slot is the ray id (pixel-tile renders: mapped from this tile's slot).
     const uint32_t ray0 = first_ray<FIRST>(pa.map, (uint32_t)slot);   // bounce 0 only
     // Pixel tiles with the reorder on: the global post-sort slot, carried per ray (seed_of).
-    in.seed = (!FIRST && seed_of) ? seed_of[slot] : (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
-    if (!INLINE) in.h = hits[slot];
     // the ray id goes out with the state loads (issued at its use, it was a round trip of its own
     // between the shading and the stores)
-    in.ray = FIRST ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
+    const uint32_t rv = FIRST ? (FIRST == 2 ? ray0 : (uint32_t)slot) : rid[slot];
+    in.ray = rv & ~kAccFlag;
+    in.acc_holds = (rv & kAccFlag) != 0;
+    in.seed = (!FIRST && seed_of) ? seed_of[slot] : (SORTED || FIRST) ? (FIRST == 2 ? ray0 : (uint32_t)slot) : in.ray;
+    if (!INLINE) in.h = hits[slot];
     if (!FIRST) {
         in.r0 = geo[(size_t)slot * 2];
         in.r1 = geo[(size_t)slot * 2 + 1];
-        in.r2 = tc[slot];
+        in.tz = tz[slot];
     }
     return in;
 }
@@ -682,7 +689,8 @@ __device__ __forceinline__ Shaded shade_from(const DevScene &S, const PassArgs &
     float closest = in.h.x;
     int index = __float_as_int(in.h.y);
     const uint32_t ray_id = in.ray;
-    V3 o, d, T, C;
+    V3 o, d, T;
+    V3 C = v3(0, 0, 0);                 // the ray's radiance lives in acc[ray] (or is 0): only this bounce's term
     if (FIRST) {
         o = S.cam;
         d = primary_dir(S, (int)(FIRST == 2 ? in.ray : (uint32_t)slot), pa);
@@ -693,12 +701,10 @@ __device__ __forceinline__ Shaded shade_from(const DevScene &S, const PassArgs &
         float tx = 1.f, ty = 1.f, tz = 1.f;
         asm volatile("" : "+v"(tx), "+v"(ty), "+v"(tz));
         T = v3(tx, ty, tz);
-        C = v3(0, 0, 0);
     } else {
         o = v3(in.r0.x, in.r0.y, in.r0.z);
         d = v3(in.r0.w, in.r1.x, in.r1.y);
-        T = v3(in.r1.z, in.r1.w, in.r2.x);
-        C = v3(in.r2.y, in.r2.z, in.r2.w);
+        T = v3(in.r1.z, in.r1.w, in.tz);
     }
     if (INLINE) {
         closest = 1e30f;
@@ -733,15 +739,20 @@ __device__ __forceinline__ Shaded shade_from(const DevScene &S, const PassArgs &
         const Mat m{v3(m0.x, m0.y, m0.z), m0.w, v3(m1.x, m1.y, m1.z), m1.w, v3(m2.x, m2.y, m2.z), m2.w};
         scatter(d, normal, m, rng, T, C, nd);
     }
-    return Shaded{no, nd, T, C, ray_id, index == -1 ? 0 : (index < S.sphere_count ? 2 : 1)};
+    return Shaded{no, nd, T, C, ray_id, index == -1 ? 0 : (index < S.sphere_count ? 2 : 1), in.acc_holds};
 }
 template <bool SORTED, int FIRST, bool INLINE = false>
 __device__ __forceinline__ Shaded shade_one(const DevScene &S, const PassArgs &pa, int slot,
-                                            const float4 *__restrict__ geo, const float4 *__restrict__ tc,
+                                            const float4 *__restrict__ geo, const float *__restrict__ tz,
                                             const uint32_t *__restrict__ rid, const float2 *__restrict__ hits,
                                             uint32_t seed_term, const uint32_t *__restrict__ seed_of = nullptr) {
-    return shade_from<SORTED, FIRST, INLINE>(S, pa, slot, shade_in<SORTED, FIRST, INLINE>(pa, slot, geo, tc, rid, hits, seed_of),
+    return shade_from<SORTED, FIRST, INLINE>(S, pa, slot, shade_in<SORTED, FIRST, INLINE>(pa, slot, geo, tz, rid, hits, seed_of),
                                              seed_term);
+}
+// A nonzero radiance term of this bounce: some component with nonzero magnitude bits (adding +-0 to the
+// radiance so far never changes it: that sum starts at +0 and so is never -0).
+__device__ __forceinline__ bool has_radiance(V3 c) {
+    return ((__float_as_uint(c.x) | __float_as_uint(c.y) | __float_as_uint(c.z)) & 0x7fffffffu) != 0;
 }
 
 // Shading for the live slots (scene.cu:376-485): environment lookup on a miss, otherwise
@@ -754,9 +765,17 @@ __device__ __forceinline__ unsigned long long match_bucket(uint32_t b, bool vali
 // counts (or null): the reorder's per-tile bucket histogram (sort_hist_kernel's output) counted here
 // as the buckets are made, so the bounce needs no histogram launch and no second read of the
 // buckets; the blocks then walk whole reorder tiles instead of 256-slot strides.
+#ifndef RT_SHADE_WPE
+#define RT_SHADE_WPE 0                // > 0: a waves-per-SIMD floor for shade_kernel (A/B only)
+#endif
+#if RT_SHADE_WPE > 0
+#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_WPE, RT_SHADE_WPE)))
+#else
+#define RT_SHADE_ATTR
+#endif
 template <bool SORTED, bool COUNT, int FIRST, bool FUSED, bool INLINE>
-__global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
-                                                       float4 *__restrict__ tc, const uint32_t *__restrict__ rid,
+__global__ __launch_bounds__(kBlock) RT_SHADE_ATTR void shade_kernel(DevScene S, PassArgs pa, float4 *__restrict__ geo,
+                                                       float *__restrict__ tz, uint32_t *__restrict__ rid,
                                                        float4 *__restrict__ acc, uint8_t *__restrict__ bkt,
                                                        const uint32_t *__restrict__ live_count,
                                                        const float2 *__restrict__ hits, uint32_t seed_term, int last,
@@ -767,26 +786,41 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DevScene S, PassArgs pa, 
     unsigned hit = 0, miss = 0, hit_sphere = 0;
     // one slot's shading and new state; returns its bucket
     auto shade_slot = [&](int slot) -> uint32_t {
-        const Shaded sh = shade_one<SORTED, FIRST, INLINE>(S, pa, slot, geo, tc, rid, hits, seed_term, seed_of);
-        const V3 no = sh.no, nd = sh.nd, T = sh.T, C = sh.C;
+        const Shaded sh = shade_one<SORTED, FIRST, INLINE>(S, pa, slot, geo, tz, rid, hits, seed_term, seed_of);
+        const V3 no = sh.no, nd = sh.nd, T = sh.T;
         miss += sh.kind == 0;
         hit += sh.kind != 0;
         hit_sphere += sh.kind == 2;
         const bool dead = is_black(T);
-        const float4 tcv = make_float4(T.z, C.x, C.y, C.z);
         if (!FUSED && !dead && !last) {     // a terminated ray's geometry is never read again
             geo[(size_t)slot * 2] = make_float4(no.x, no.y, no.z, nd.x);
             geo[(size_t)slot * 2 + 1] = make_float4(nd.y, nd.z, T.x, T.y);
+            tz[slot] = T.z;
         }
-        if (dead || last) {
-            // scattered 16-B writes (rays terminate in sorted, not ray-id, order): nontemporal, so
-            // the radiance lines do not displace the scene records the trace kernels re-read from
-            // L2 (round 4: later-bounce shade 1.73 -> 1.45 ms alone, teapot 20 steps 6.73 -> 6.41
-            // ms/pass; the same hint on the coalesced ray-state, hit and bucket traffic: +1-2 %)
+        // The radiance (the reference's `collected`, scene.cu:383,417) is not carried with the ray: a bounce's
+        // term goes to acc[ray id] when it is nonzero or the ray ends, added to what acc holds (kAccFlag)
+        // in the reference's order -- the same sums, 12 B less state per live ray in every shade and reorder.
+        const bool term = has_radiance(sh.C);
+        if (dead || last || term) {
+            V3 C = sh.C;
+            if (sh.acc_holds) {
+                const float4 a = acc[sh.ray];
+                C = v3(a.y, a.z, a.w) + sh.C;
+            }
             typedef float f4v __attribute__((ext_vector_type(4)));
-            __builtin_nontemporal_store(f4v{tcv.x, tcv.y, tcv.z, tcv.w}, reinterpret_cast<f4v *>(acc + sh.ray));
+            if (dead || last)
+                // scattered 16-B writes (rays terminate in sorted, not ray-id, order): nontemporal, so
+                // the radiance lines do not displace the scene records the trace kernels re-read from
+                // L2 (round 4: later-bounce shade 1.73 -> 1.45 ms alone, teapot 20 steps 6.73 -> 6.41
+                // ms/pass; the same hint on the coalesced ray-state, hit and bucket traffic: +1-2 %)
+                __builtin_nontemporal_store(f4v{T.z, C.x, C.y, C.z}, reinterpret_cast<f4v *>(acc + sh.ray));
+            else
+                acc[sh.ray] = make_float4(T.z, C.x, C.y, C.z);   // read back at a later bounce
         }
-        else if (!FUSED) tc[slot] = tcv;   // FUSED: the reorder replays the shading instead
+        // the flag rides in the ray id, which the reorder moves (at bounce 0 written for every ray: the
+        // reorder's bounce-0 scatter reads it there; FUSED: the replay sets it)
+        if (!FUSED && !dead && !last && (FIRST || (term && !sh.acc_holds)))
+            rid[slot] = sh.ray | (term || sh.acc_holds ? kAccFlag : 0u);
         const uint32_t bk = dead ? kDead : (SORTED ? bucket_of(no, nd, S.min_coord, S.inv_dim) : 0u);
         if (!last) bkt[slot] = (uint8_t)bk;
         return bk;
@@ -962,12 +996,12 @@ __global__ __launch_bounds__(kBlock) void sort_scan_kernel(const uint32_t *__res
 template <int FIRST_SRC>
 __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__restrict__ bkt_in,
                                                               const float4 *__restrict__ geo_in,
-                                                              const float4 *__restrict__ tc_in,
+                                                              const float *__restrict__ tz_in,
                                                               const uint32_t *__restrict__ rid_in,
                                                               const uint32_t *__restrict__ live_count, int tiles,
                                                               const uint32_t *__restrict__ offsets,
                                                               const uint32_t *__restrict__ totals,
-                                                              float4 *__restrict__ geo_out, float4 *__restrict__ tc_out,
+                                                              float4 *__restrict__ geo_out, float *__restrict__ tz_out,
                                                               uint32_t *__restrict__ rid_out, SlotMap map,
                                                               const uint32_t *__restrict__ gslot_in = nullptr,
                                                               const uint32_t *__restrict__ newpos = nullptr,
@@ -990,13 +1024,14 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
         const bool valid = item < n;
         const uint32_t b = valid ? bkt_in[item] : 0u;
         const bool move = valid && b != kDead;
-        float4 g0 = make_float4(0, 0, 0, 0), g1 = g0, t = g0;
+        float4 g0 = make_float4(0, 0, 0, 0), g1 = g0;
+        float t = 0;
         uint32_t id = 0;
         if (move) {                     // issued before the ranking so the loads overlap it
             g0 = geo_in[(size_t)item * 2];
             g1 = geo_in[(size_t)item * 2 + 1];
-            t = tc_in[item];
-            id = FIRST_SRC ? first_ray<FIRST_SRC>(map, (uint32_t)item) : rid_in[item];
+            t = tz_in[item];
+            id = rid_in[item];          // bounce 0: written by the shade kernel (the ray index + kAccFlag)
         }
         uint32_t gs = 0;
         if (gslot_out && move) gs = newpos[FIRST_SRC ? first_ray<FIRST_SRC>(map, (uint32_t)item) : gslot_in[item]];
@@ -1009,7 +1044,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const uint8_t *__r
             for (int k = 0; k < wave; k++) pos += wcount[k][b];
             geo_out[(size_t)pos * 2] = g0;
             geo_out[(size_t)pos * 2 + 1] = g1;
-            tc_out[pos] = t;
+            tz_out[pos] = t;
             rid_out[pos] = id;
             if (gslot_out) gslot_out[pos] = gs;
         }
@@ -1156,14 +1191,14 @@ template <bool SORTED, int FIRST, bool INLINE>
 __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, PassArgs pa,
                                                                     const uint8_t *__restrict__ bkt_in,
                                                                     const float4 *__restrict__ geo_in,
-                                                                    const float4 *__restrict__ tc_in,
+                                                                    const float *__restrict__ tz_in,
                                                                     const uint32_t *__restrict__ rid_in,
                                                                     const float2 *__restrict__ hits, uint32_t seed_term,
                                                                     const uint32_t *__restrict__ live_count, int tiles,
                                                                     const uint32_t *__restrict__ offsets,
                                                                     const uint32_t *__restrict__ totals,
                                                                     float4 *__restrict__ geo_out,
-                                                                    float4 *__restrict__ tc_out,
+                                                                    float *__restrict__ tz_out,
                                                                     uint32_t *__restrict__ rid_out) {
     const int n = (int)*live_count;
     __shared__ uint32_t run[kBuckets];
@@ -1182,7 +1217,7 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
             const uint32_t b = valid ? bkt_in[item] : 0u;
             const bool move = valid && b != kDead;
             Shaded sh{};
-            if (move) sh = shade_one<SORTED, FIRST, INLINE>(S, pa, item, geo_in, tc_in, rid_in, hits, seed_term);
+            if (move) sh = shade_one<SORTED, FIRST, INLINE>(S, pa, item, geo_in, tz_in, rid_in, hits, seed_term);
             const unsigned long long peers = match_bucket(b, valid);
             const uint32_t rank = rank_below(peers);
             if (valid && rank == 0) wcount[wave][b] = (uint32_t)__popcll(peers);
@@ -1192,8 +1227,9 @@ __global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, 
                 for (int k = 0; k < wave; k++) pos += wcount[k][b];
                 geo_out[(size_t)pos * 2] = make_float4(sh.no.x, sh.no.y, sh.no.z, sh.nd.x);
                 geo_out[(size_t)pos * 2 + 1] = make_float4(sh.nd.y, sh.nd.z, sh.T.x, sh.T.y);
-                tc_out[pos] = make_float4(sh.T.z, sh.C.x, sh.C.y, sh.C.z);
-                rid_out[pos] = sh.ray;
+                tz_out[pos] = sh.T.z;
+                // the shade kernel has added a nonzero term into acc[ray]: from now on acc holds the radiance
+                rid_out[pos] = sh.ray | (has_radiance(sh.C) || sh.acc_holds ? kAccFlag : 0u);
             }
             __syncthreads();
             if (threadIdx.x < kBuckets) {
@@ -1357,9 +1393,11 @@ struct InitTimer {
 struct PassCtx {
     hipStream_t stream = nullptr;
     // Ray state in slot order, ping-ponged by the reorder (sort off: one copy, slot = ray id):
-    // geo = 2 x float4 {o.xyz, d.x} {d.yz, T.xy}, tc = {T.z, C.xyz}, rid = ray id.  acc[ray id]
-    // receives a ray's {T.z, C} when it terminates or after the last bounce (sort on only).
-    DevBuf<float4> geo[2], tc[2], acc;
+    // geo = 2 x float4 {o.xyz, d.x} {d.yz, T.xy}, tz = T.z, rid = ray id (+ kAccFlag).  acc[ray id]
+    // holds {T.z, C}: the radiance once a bounce added a nonzero term, and finally when the ray terminates
+    // or after the last bounce.
+    DevBuf<float4> geo[2], acc;
+    DevBuf<float> tz[2];
     DevBuf<uint32_t> rid[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
     DevBuf<uint8_t> bkt;
     DevBuf<float2> hits;
@@ -1618,7 +1656,7 @@ struct rt_renderer {
         const int tiles = tile_stride(max_rays);
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
         // than half of the free device memory holds (1080p: ~2.9 GB per context).
-        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 16 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0)) +
+        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 4 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0)) +
                                  (size_t)trace_blocks_max * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
         size_t mem_free = 0, mem_total = 0;
         HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
@@ -1642,7 +1680,7 @@ struct rt_renderer {
             if ((rc = c.open())) return rc;
             for (int q = 0; q < 2; q++) {
                 if ((rc = c.geo[q].alloc((size_t)max_rays * 2))) return rc;
-                if ((rc = c.tc[q].alloc((size_t)max_rays))) return rc;
+                if ((rc = c.tz[q].alloc((size_t)max_rays))) return rc;
                 if ((rc = c.rid[q].alloc((size_t)max_rays))) return rc;
             }
             if ((rc = c.bkt.alloc((size_t)max_rays))) return rc;
@@ -1750,15 +1788,15 @@ struct rt_renderer {
         if (em) HIPCHK(hipEventRecord(em, st));                                                                  \
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
-                               ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,  \
+                               ds, pa, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,  \
                                seed_term, (int)last, ctr.p, nullptr, hist, tiles);                               \
         else if (fused || b <= fused_upto)                                                                       \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, false>), dim3(sgrid), dim3(kBlock), 0, \
-                               st, ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
+                               st, ds, pa, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
                                seed_term, (int)last, ctr.p, nullptr, hist, tiles);                               \
         else                                                                                                     \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, false, false>), dim3(sgrid), dim3(kBlock), 0, \
-                               st, ds, pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
+                               st, ds, pa, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
                                seed_term, (int)last, ctr.p, nullptr, hist, tiles);                               \
     } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
@@ -1793,8 +1831,8 @@ struct rt_renderer {
                 if (fused || b <= fused_upto) {
 #define RT_FSC2(SO, FI, IN)                                                                                      \
     hipLaunchKernelGGL((sort_scatter_shade_kernel<SO, FI, IN>), dim3(sort_grid), dim3(kBlock), 0, st, ds, pa,     \
-                       c.bkt.p, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.hits.p, seed_term, lv, tiles,          \
-                       c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p)
+                       c.bkt.p, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.hits.p, seed_term, lv, tiles,          \
+                       c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p, c.tz[1 - cur].p, c.rid[1 - cur].p)
 #define RT_FSC(SO, FI) do { if (inline_hits) RT_FSC2(SO, FI, true); else RT_FSC2(SO, FI, false); } while (0)
                     if (sort) {
                         if (b == 0) RT_FSC(true, 1); else RT_FSC(true, 0);
@@ -1805,16 +1843,16 @@ struct rt_renderer {
 #undef RT_FSC2
                 } else if (b == 0 && tiled())
                     hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
+                                       c.tz[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                       c.geo[1 - cur].p, c.tz[1 - cur].p, c.rid[1 - cur].p, pa.map);
                 else if (b == 0)
                     hipLaunchKernelGGL(sort_scatter_kernel<1>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
+                                       c.tz[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                       c.geo[1 - cur].p, c.tz[1 - cur].p, c.rid[1 - cur].p, pa.map);
                 else
                     hipLaunchKernelGGL(sort_scatter_kernel<0>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                                       c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
-                                       c.geo[1 - cur].p, c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map);
+                                       c.tz[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p,
+                                       c.geo[1 - cur].p, c.tz[1 - cur].p, c.rid[1 - cur].p, pa.map);
                 HIPCHK(hipGetLastError());
                 if (pass_events) HIPCHK(hipEventRecord(s1, st));
                 cur = 1 - cur;
@@ -1910,13 +1948,13 @@ struct rt_renderer {
             hipLaunchKernelGGL((trace_kernel<true, COUNT, 2>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
                                c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
             hipLaunchKernelGGL((shade_kernel<true, COUNT, 2, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
-                               pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
+                               pa, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
                                seed_term, last, ctr.p, nullptr);                                                   \
         } else {                                                                                                   \
             hipLaunchKernelGGL((trace_kernel<true, COUNT, 0>), dim3(tgrid), dim3(kBlock), 0, st, ds, pa,            \
                                c.geo[cur].p, lv, q, c.hits.p, c.overflow.p, ctr.p, nullptr);                       \
             hipLaunchKernelGGL((shade_kernel<true, COUNT, 0, false, false>), dim3(sgrid), dim3(kBlock), 0, st, ds, \
-                               pa, c.geo[cur].p, c.tc[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
+                               pa, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,         \
                                seed_term, last, ctr.p, c.gslot[cur].p);                                            \
         }                                                                                                          \
     } while (0)
@@ -1984,12 +2022,12 @@ struct rt_renderer {
                            c.sort_offsets.p, c.sort_totals.p, c.live.p + b + 1);
         if (b == 0)
             hipLaunchKernelGGL(sort_scatter_kernel<2>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                               c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p,
-                               c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, c.gslot[cur].p, c.newpos.p, c.gslot[1 - cur].p);
+                               c.tz[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p,
+                               c.tz[1 - cur].p, c.rid[1 - cur].p, pa.map, c.gslot[cur].p, c.newpos.p, c.gslot[1 - cur].p);
         else
             hipLaunchKernelGGL(sort_scatter_kernel<0>, dim3(sort_grid), dim3(kBlock), 0, st, c.bkt.p, c.geo[cur].p,
-                               c.tc[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p,
-                               c.tc[1 - cur].p, c.rid[1 - cur].p, pa.map, c.gslot[cur].p, c.newpos.p, c.gslot[1 - cur].p);
+                               c.tz[cur].p, c.rid[cur].p, lv, tiles, c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p,
+                               c.tz[1 - cur].p, c.rid[1 - cur].p, pa.map, c.gslot[cur].p, c.newpos.p, c.gslot[1 - cur].p);
         HIPCHK(hipGetLastError());
         c.t_cur = 1 - cur;
         return RT_OK;
