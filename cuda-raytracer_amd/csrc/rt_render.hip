@@ -766,7 +766,19 @@ __device__ __forceinline__ unsigned long long match_bucket(uint32_t b, bool vali
 // as the buckets are made, so the bounce needs no histogram launch and no second read of the
 // buckets; the blocks then walk whole reorder tiles instead of 256-slot strides.
 #ifndef RT_SHADE_WPE
-#define RT_SHADE_WPE 0                // > 0: a waves-per-SIMD floor for shade_kernel (A/B only)
+// waves-per-SIMD floor for shade_kernel: its scalar registers alone held it at 7 (101-106 SGPRs); at 8 (round 5,
+// A/B after the slim state): frame -0.9 %, lamp -0.5 %, cornell_plus -1.8 %, 20 steps +-0.3 %
+#define RT_SHADE_WPE 8
+#endif
+#ifndef RT_REPLAY_WPE
+// the same for the fused replay (sort_scatter_shade_kernel): 6 waves by its 75 VGPRs; at 8 (a 20-B spill; round 5 A/B):
+// teapot 20 steps -2.1 %, frame -0.5 %, cornell_plus -1.5 %, spheres +-0
+#define RT_REPLAY_WPE 8
+#endif
+#if RT_REPLAY_WPE > 0
+#define RT_REPLAY_ATTR __attribute__((amdgpu_waves_per_eu(RT_REPLAY_WPE, RT_REPLAY_WPE)))
+#else
+#define RT_REPLAY_ATTR
 #endif
 #if RT_SHADE_WPE > 0
 #define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_WPE, RT_SHADE_WPE)))
@@ -1188,7 +1200,7 @@ __global__ void set_count_kernel(uint32_t *__restrict__ dst, uint32_t v, const u
 // deterministic) and writes the new state straight to its sorted slot, saving the shade
 // kernel's 48-B state write and the plain scatter's 48-B read per live ray.
 template <bool SORTED, int FIRST, bool INLINE>
-__global__ __launch_bounds__(kBlock) void sort_scatter_shade_kernel(DevScene S, PassArgs pa,
+__global__ __launch_bounds__(kBlock) RT_REPLAY_ATTR void sort_scatter_shade_kernel(DevScene S, PassArgs pa,
                                                                     const uint8_t *__restrict__ bkt_in,
                                                                     const float4 *__restrict__ geo_in,
                                                                     const float *__restrict__ tz_in,
