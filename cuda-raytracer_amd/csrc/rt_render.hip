@@ -793,7 +793,10 @@ __global__ __launch_bounds__(kBlock) RT_SHADE_ATTR void shade_kernel(DevScene S,
                                                        const float2 *__restrict__ hits, uint32_t seed_term, int last,
                                                        Counters *__restrict__ ctr,
                                                        const uint32_t *__restrict__ seed_of = nullptr,
-                                                       uint32_t *__restrict__ counts = nullptr, int tiles = 0) {
+                                                       uint32_t *__restrict__ counts = nullptr, int tiles = 0,
+                                                       int home = 0) {
+    // home (bounce 0 of a sorted render whose bounce-0 reorder is the fused replay): a surviving ray's radiance
+    // lives at its home index (sort_scatter_shade_kernel), so its term here is left to the replay
     const int L = (int)__builtin_amdgcn_readfirstlane(*live_count);
     unsigned hit = 0, miss = 0, hit_sphere = 0;
     // one slot's shading and new state; returns its bucket
@@ -813,10 +816,11 @@ __global__ __launch_bounds__(kBlock) RT_SHADE_ATTR void shade_kernel(DevScene S,
         // term goes to acc[ray id] when it is nonzero or the ray ends, added to what acc holds (kAccFlag)
         // in the reference's order -- the same sums, 12 B less state per live ray in every shade and reorder.
         const bool term = has_radiance(sh.C);
-        if (dead || last || term) {
+        if (dead || last || (term && !(FIRST && home))) {
             V3 C = sh.C;
+            const uint32_t dst = sh.ray;      // the ray id, or (Renderer::home) its home index
             if (sh.acc_holds) {
-                const float4 a = acc[sh.ray];
+                const float4 a = acc[dst];
                 C = v3(a.y, a.z, a.w) + sh.C;
             }
             typedef float f4v __attribute__((ext_vector_type(4)));
@@ -825,9 +829,9 @@ __global__ __launch_bounds__(kBlock) RT_SHADE_ATTR void shade_kernel(DevScene S,
                 // the radiance lines do not displace the scene records the trace kernels re-read from
                 // L2 (round 4: later-bounce shade 1.73 -> 1.45 ms alone, teapot 20 steps 6.73 -> 6.41
                 // ms/pass; the same hint on the coalesced ray-state, hit and bucket traffic: +1-2 %)
-                __builtin_nontemporal_store(f4v{T.z, C.x, C.y, C.z}, reinterpret_cast<f4v *>(acc + sh.ray));
+                __builtin_nontemporal_store(f4v{T.z, C.x, C.y, C.z}, reinterpret_cast<f4v *>(acc + dst));
             else
-                acc[sh.ray] = make_float4(T.z, C.x, C.y, C.z);   // read back at a later bounce
+                acc[dst] = make_float4(T.z, C.x, C.y, C.z);   // read back at a later bounce
         }
         // the flag rides in the ray id, which the reorder moves (at bounce 0 written for every ray: the
         // reorder's bounce-0 scatter reads it there; FUSED: the replay sets it)
@@ -1211,7 +1215,16 @@ __global__ __launch_bounds__(kBlock) RT_REPLAY_ATTR void sort_scatter_shade_kern
                                                                     const uint32_t *__restrict__ totals,
                                                                     float4 *__restrict__ geo_out,
                                                                     float *__restrict__ tz_out,
-                                                                    uint32_t *__restrict__ rid_out) {
+                                                                    uint32_t *__restrict__ rid_out,
+                                                                    float4 *__restrict__ acc = nullptr,
+                                                                    uint32_t *__restrict__ home_of = nullptr,
+                                                                    uint32_t home_base = 0) {
+    // home_of (bounce 0, sort on): each surviving ray gets the home index home_base + its bounce-1 slot, which it
+    // carries as its rid from now on: its radiance goes to acc[home], so the rays that terminate at bounce 1 -- most
+    // of them -- store it coalesced (in ray-id order they were 16-B stores to scattered lines, each a partial HBM
+    // line write).  A ray terminated at bounce 0 keeps acc[ray id] (written by the shade kernel, in slot = ray-id
+    // order).  home_of[ray id] tells the accumulation where to read.
+    const bool homes = FIRST == 1 && home_of != nullptr;
     const int n = (int)*live_count;
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t wcount[kBlock / 64][kBuckets];
@@ -1240,8 +1253,15 @@ __global__ __launch_bounds__(kBlock) RT_REPLAY_ATTR void sort_scatter_shade_kern
                 geo_out[(size_t)pos * 2] = make_float4(sh.no.x, sh.no.y, sh.no.z, sh.nd.x);
                 geo_out[(size_t)pos * 2 + 1] = make_float4(sh.nd.y, sh.nd.z, sh.T.x, sh.T.y);
                 tz_out[pos] = sh.T.z;
-                // the shade kernel has added a nonzero term into acc[ray]: from now on acc holds the radiance
-                rid_out[pos] = sh.ray | (has_radiance(sh.C) || sh.acc_holds ? kAccFlag : 0u);
+                const uint32_t id = homes ? home_base + pos : sh.ray;
+                if (homes) {
+                    home_of[item] = id;
+                    if (has_radiance(sh.C)) acc[id] = make_float4(sh.T.z, sh.C.x, sh.C.y, sh.C.z);
+                }
+                // the shade kernel (home: this kernel) has added a nonzero term into acc[id]: from now on acc holds the radiance
+                rid_out[pos] = id | (has_radiance(sh.C) || sh.acc_holds ? kAccFlag : 0u);
+            } else if (homes && valid) {
+                home_of[item] = (uint32_t)item;
             }
             __syncthreads();
             if (threadIdx.x < kBuckets) {
@@ -1262,16 +1282,20 @@ __global__ __launch_bounds__(kBlock) RT_REPLAY_ATTR void sort_scatter_shade_kern
 constexpr int kAccPixels = 64;
 // TILED: the block's pixels are tile pixels (this owner's row stripes back to back), mapped to
 // image pixels by `pix`; otherwise pixels of the whole image.
+// home_of (sort on, fused bounce-0 reorder): sample e's radiance is at tc[home_of[e]] (sort_scatter_shade_kernel).
 template <bool TILED>
 __global__ __launch_bounds__(kBlock) void accumulate_kernel(const float4 *__restrict__ tc, int rtc, int pixels,
-                                                            float *__restrict__ sums, SlotMap pix) {
+                                                            float *__restrict__ sums, SlotMap pix,
+                                                            const uint32_t *__restrict__ home_of = nullptr) {
     __shared__ float col[kAccPixels * 20 * 3];
     const int p0 = blockIdx.x * kAccPixels;
     const int np = min(kAccPixels, pixels - p0);
     const int n = np * rtc;
     const float4 *src = tc + (size_t)p0 * rtc;
     for (int e = threadIdx.x; e < n; e += kBlock) {
-        const float4 c = TILED ? tc[(size_t)pix.ray((uint32_t)(p0 + e / rtc)) * rtc + e % rtc] : src[e];
+        const float4 c = TILED     ? tc[(size_t)pix.ray((uint32_t)(p0 + e / rtc)) * rtc + e % rtc]
+                         : home_of ? tc[home_of[(size_t)p0 * rtc + e]]
+                                   : src[e];
         col[e * 3] = c.y;
         col[e * 3 + 1] = c.z;
         col[e * 3 + 2] = c.w;
@@ -1413,6 +1437,9 @@ struct PassCtx {
     DevBuf<uint32_t> rid[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
     DevBuf<uint8_t> bkt;
     DevBuf<float2> hits;
+    // Renderer::home: acc holds 2 x max_rays entries (ray ids below max_rays for rays terminated at bounce 0,
+    // home indices from max_rays on for the rest); home_of[ray id] = where the ray's radiance is
+    DevBuf<uint32_t> home_of;
     DevBuf<float> psum;               // this pass's per-pixel sums (when the caller gives no buffer)
     // pixel tiles with the reorder on: global slot per ray (ping-pong with the state), the global
     // bucket bytes (exchanged) and this owner's own bytes, their ranks, the global live count
@@ -1462,7 +1489,7 @@ struct rt_renderer {
     // per-bounce HIP events for rt_stats.process_ms / sort_ms (rt_renderer_set_event_timing): four
     // marker packets per bounce in every pass's stream; off, a frame runs ~2 % faster
     bool pass_events = true;
-    // Fused reorder: shade writes only buckets and the scatter replays the shading (no 48-B state
+    // Fused reorder: shade writes only buckets and the scatter replays the shading (no 36-B state
     // round trip per live ray).  It pays where the bounce is HBM-streaming bound: every bounce of
     // a scene with cheap traversal (spheres: 3.82 -> 3.52 ms/pass), and bounce 0 of a big one
     // (all rays live, primary rays cheap to replay: teapot 7.68 -> 7.49, lamp 15.33 -> 15.10);
@@ -1474,6 +1501,10 @@ struct rt_renderer {
     // shade/reorder (INLINE), saving the hit round trip and the trace launch per bounce.
     bool inline_hits = false;
     int fused_upto = -1;              // fused reorder at bounces <= this (when not `fused`)
+    // Sort on with the fused bounce-0 reorder: a surviving ray's radiance goes to acc[home] (home = max_rays + its
+    // bounce-1 slot) instead of acc[ray id] (sort_scatter_shade_kernel).  RTAMD_HOME=0: ray ids throughout.
+    bool home = false;
+    uint32_t home_base = 0;
     int width = 0, height = 0, spp = 0, bounces = 0;
     DevScene ds{};
     DevBuf<float4> spheres, tris, mats, nodes;
@@ -1666,9 +1697,13 @@ struct rt_renderer {
         trace_blocks_max = std::max(1, cus * std::max(1, per_cu));
         trace_blocks = trace_blocks_max;
         const int tiles = tile_stride(max_rays);
+        home = sort && !tiled() && bounces >= 2 && (fused || fused_upto >= 0);
+        if (const char *e = std::getenv("RTAMD_HOME")) home = home && std::atoi(e) != 0;
+        home_base = (uint32_t)max_rays;
         // Passes in flight: up to kInflight, as many as the frame has, and no more contexts
         // than half of the free device memory holds (1080p: ~2.9 GB per context).
-        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 4 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0)) +
+        const size_t ctx_bytes = (size_t)max_rays * (2 * (32 + 4 + 4) + 16 + 1 + 8 + (tsort() ? 2 * 4 + 4 + 2 : 0) +
+                                                     (home ? 16 + 4 : 0)) +
                                  (size_t)trace_blocks_max * kBlock * 8 * (kStackMax - kStackLds) + ((size_t)1 << 20);
         size_t mem_free = 0, mem_total = 0;
         HIPCHK(hipMemGetInfo(&mem_free, &mem_total));
@@ -1696,7 +1731,8 @@ struct rt_renderer {
                 if ((rc = c.rid[q].alloc((size_t)max_rays))) return rc;
             }
             if ((rc = c.bkt.alloc((size_t)max_rays))) return rc;
-            if ((rc = c.acc.alloc((size_t)max_rays))) return rc;
+            if ((rc = c.acc.alloc((size_t)max_rays * (home ? 2 : 1)))) return rc;
+            if (home && (rc = c.home_of.alloc((size_t)max_rays))) return rc;
             if ((rc = c.sort_counts.alloc((size_t)kBuckets * tiles))) return rc;
             if ((rc = c.sort_offsets.alloc((size_t)kBuckets * tiles))) return rc;
             if ((rc = c.sort_totals.alloc(kBuckets))) return rc;
@@ -1801,15 +1837,15 @@ struct rt_renderer {
         if (inline_hits)                                                                                         \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, true>), dim3(sgrid), dim3(kBlock), 0, st,\
                                ds, pa, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,  \
-                               seed_term, (int)last, ctr.p, nullptr, hist, tiles);                               \
+                               seed_term, (int)last, ctr.p, nullptr, hist, tiles, (int)(home && b == 0));        \
         else if (fused || b <= fused_upto)                                                                       \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, true, false>), dim3(sgrid), dim3(kBlock), 0, \
                                st, ds, pa, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
-                               seed_term, (int)last, ctr.p, nullptr, hist, tiles);                               \
+                               seed_term, (int)last, ctr.p, nullptr, hist, tiles, (int)(home && b == 0));        \
         else                                                                                                     \
             hipLaunchKernelGGL((shade_kernel<SORTED, COUNT, FIRST, false, false>), dim3(sgrid), dim3(kBlock), 0, \
                                st, ds, pa, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.acc.p, c.bkt.p, lv, c.hits.p,      \
-                               seed_term, (int)last, ctr.p, nullptr, hist, tiles);                               \
+                               seed_term, (int)last, ctr.p, nullptr, hist, tiles, (int)(home && b == 0));        \
     } while (0)
 #define RT_PROCESS(SORTED, COUNT)                                                                                \
     do {                                                                                                         \
@@ -1844,7 +1880,8 @@ struct rt_renderer {
 #define RT_FSC2(SO, FI, IN)                                                                                      \
     hipLaunchKernelGGL((sort_scatter_shade_kernel<SO, FI, IN>), dim3(sort_grid), dim3(kBlock), 0, st, ds, pa,     \
                        c.bkt.p, c.geo[cur].p, c.tz[cur].p, c.rid[cur].p, c.hits.p, seed_term, lv, tiles,          \
-                       c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p, c.tz[1 - cur].p, c.rid[1 - cur].p)
+                       c.sort_offsets.p, c.sort_totals.p, c.geo[1 - cur].p, c.tz[1 - cur].p, c.rid[1 - cur].p,    \
+                       c.acc.p, home && b == 0 ? c.home_of.p : nullptr, home_base)
 #define RT_FSC(SO, FI) do { if (inline_hits) RT_FSC2(SO, FI, true); else RT_FSC2(SO, FI, false); } while (0)
                     if (sort) {
                         if (b == 0) RT_FSC(true, 1); else RT_FSC(true, 0);
@@ -1876,7 +1913,7 @@ struct rt_renderer {
             HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
         } else if (!tiled()) {
             hipLaunchKernelGGL(accumulate_kernel<false>, dim3((unsigned)((pixels + kAccPixels - 1) / kAccPixels)),
-                               dim3(kBlock), 0, st, c.acc.p, rtc, (int)pixels, sums, pix);
+                               dim3(kBlock), 0, st, c.acc.p, rtc, (int)pixels, sums, pix, home ? c.home_of.p : nullptr);
         } else {
             // other owners' pixels stay 0 in this render's pass sums
             HIPCHK(hipMemsetAsync(sums, 0, (size_t)pixels * 3 * sizeof(float), st));
