@@ -232,8 +232,19 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
     const size_t sl = (px3 + world - 1) / world;      // floats per owner slice (last one padded)
     const size_t pitch = sl * world;                  // pass buffer rows padded to N equal slices
     const int R = (P + world - 1) / world;            // rounds: one pass per device each
-    // rounds per exchange: all of them up to 16 (the renderer's passes in flight next to RCCL)
-    const int chunk = std::max(1, std::min(R, 16));
+    // One device: the all-to-all and the gather are the identity (every slice is its own), so they are skipped
+    // and the adds read buf directly, as the torch.distributed path does at N = 1.  RTAMD_XCHG_IDENTITY=0 runs
+    // them through RCCL anyway (the N = 1 tests keep the collectives exercised).
+    const char *ide = std::getenv("RTAMD_XCHG_IDENTITY");
+    const bool identity = world == 1 && !lb && (!ide || std::atoi(ide) != 0);
+    // Rounds per renderer call: all of them, so that the renderer keeps its passes in flight across the whole
+    // share (between calls it drains: a 26-pass share ran 6.40 ms/pass in calls of 16 passes against 5.91 for
+    // one plain run), up to 16 GB of pass buffers (buf + recv: 1080p, 320 rounds).  The chunk must be the same
+    // on every device (it fixes the collective sequence): it depends only on R and the image size.
+    // RTAMD_XCHG_CHUNK forces a smaller one (the tests' multi-call cases).
+    const size_t round_bytes = pitch * sizeof(float) * 2;
+    int chunk = std::max(1, std::min<int>(R, (int)std::min<size_t>((size_t)1 << 30, ((size_t)16 << 30) / round_bytes)));
+    if (const char *ce = std::getenv("RTAMD_XCHG_CHUNK")) chunk = std::max(1, std::min(chunk, std::atoi(ce)));
     rt_opts o = *base;
     o.device = st.device;
     o.device_count = 0;
@@ -265,9 +276,14 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
     // the owners add the pass slices themselves: no framebuffer add chain across the pass streams
     rc = rt_renderer_set_accumulate(ren, 0);
     if (rc) return rc;
+    // no per-bounce HIP events (four marker packets per bounce in every pass's stream, ~2 %), as in bench.py's
+    // timed steps: the multi-device stats carry no process_ms / sort_ms / trace_ms (RTAMD_MULTI_EVENTS=1 keeps them)
+    const char *mev = std::getenv("RTAMD_MULTI_EVENTS");
+    rc = rt_renderer_set_event_timing(ren, mev && std::atoi(mev) != 0);
+    if (rc) return rc;
     float *&buf = g.bufs[0], *&recv = g.bufs[1], *&slice = g.bufs[2];
     MHIP(hipMalloc(reinterpret_cast<void **>(&buf), (size_t)chunk * pitch * sizeof(float)));
-    MHIP(hipMalloc(reinterpret_cast<void **>(&recv), (size_t)chunk * pitch * sizeof(float)));
+    if (!identity) MHIP(hipMalloc(reinterpret_cast<void **>(&recv), (size_t)chunk * pitch * sizeof(float)));
     MHIP(hipMalloc(reinterpret_cast<void **>(&slice), (st.rank == 0 ? pitch : sl) * sizeof(float)));
     MHIP(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
     MHIP(hipMemsetAsync(buf, 0, (size_t)chunk * pitch * sizeof(float), g.s));   // padding stays 0
@@ -306,6 +322,18 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
         // rounds of the chunk where this device has no pass send stale rows, which the owners'
         // adds skip (pass src + N*k does not exist)
         auto t0 = clk::now();
+        // RTAMD_TIMING: when the exchange groups ran on the device (events around each group's adds)
+        std::vector<hipEvent_t> gev;
+        const bool gtime = std::getenv("RTAMD_TIMING") != nullptr;
+        auto gmark = [&]() -> int {
+            if (!gtime) return RT_OK;
+            hipEvent_t e = nullptr;
+            MHIP(hipEventCreate(&e));
+            gev.push_back(e);
+            MHIP(hipEventRecord(e, g.s));
+            return RT_OK;
+        };
+        if (int rc_ = gmark()) return rc_;
         for (int j0 = 0; j0 < m; j0 += xr) {
             const int j1 = std::min(m, j0 + xr);
             if (overlap)
@@ -313,7 +341,9 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
                     rc = rt_renderer_wait_pass(ren, j, g.s);
                     if (rc) return rc;
                 }
-            if (lb) {
+            if (int rc_ = gmark()) return rc_;     // the group's passes are done
+            if (identity) {
+            } else if (lb) {
                 if (int rc2 = lb->alltoall(st.rank, buf, recv, j0, j1, pitch, sl, g.s))
                     return rtamd::fail(rc2, "loopback exchange failed");
             } else {
@@ -323,8 +353,9 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
                 MNCCL(ncclGroupEnd());
             }
             hipLaunchKernelGGL(add_slices_kernel, dim3((unsigned)((sl + 255) / 256)), dim3(256), 0, g.s, slice,
-                               recv + (size_t)j0 * pitch, sl, world, j1 - j0, k0 + j0, P);
+                               (identity ? buf : recv) + (size_t)j0 * pitch, sl, world, j1 - j0, k0 + j0, P);
             MHIP(hipGetLastError());
+            if (int rc_ = gmark()) return rc_;     // its adds are done
         }
         if (mine > 0 && overlap) {
             // the passes render on the renderer's own streams, which no collective waits behind:
@@ -336,15 +367,29 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
             t0 = clk::now();            // exchange_ms: what the render did not hide
         }
         // the next chunk's render overwrites buf: the exchange must have read it
+        const auto tf = clk::now();
         MWAIT(g.s);
         st.exchange_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        if (gtime) {
+            std::string line;
+            for (size_t k = 1; k < gev.size(); k++) {
+                float ms = 0;
+                MHIP(hipEventElapsedTime(&ms, gev[0], gev[k]));
+                line += (k % 2 ? " ready " : " added ") + std::to_string(ms);
+            }
+            for (hipEvent_t e : gev) (void)hipEventDestroy(e);
+            std::fprintf(stderr, "rt_multi device %d chunk at round %d: exchange groups (ms after the chunk's enqueue):%s; "
+                         "host wait after the render %.2f ms\n", st.rank, k0, line.c_str(),
+                         std::chrono::duration<double, std::milli>(clk::now() - tf).count());
+        }
     }
     const double loop_ms = std::chrono::duration<double, std::milli>(clk::now() - loop0).count();
+    const double unhidden_ms = st.exchange_ms;
     const auto t0 = clk::now();
     // gather the finished slices to the root (in place: the root's own slice is block 0)
     if (lb) {
         if (int rc2 = lb->gather(st.rank, slice, sl, g.s)) return rtamd::fail(rc2, "loopback gather failed");
-    } else {
+    } else if (!identity) {
         MNCCL(ncclGather(slice, slice, sl, ncclFloat32, 0, comm, g.s));
     }
     if (st.rank == 0) MHIP(hipMemcpyAsync(fb_out, slice, px3 * sizeof(float), hipMemcpyDeviceToHost, g.s));
@@ -353,7 +398,7 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
     if (std::getenv("RTAMD_TIMING"))
         std::fprintf(stderr, "rt_multi device %d: %d passes rendered and exchanged in %.2f ms (exchange not hidden: %.2f ms, "
                      "%s), then gather + framebuffer to the host %.2f ms\n", st.rank, (int)st.stats.passes, loop_ms,
-                     st.exchange_ms, overlap ? "overlapped" : "after each chunk",
+                     unhidden_ms, overlap ? "overlapped" : "after each chunk",
                      std::chrono::duration<double, std::milli>(clk::now() - t0).count());
     run.ok = true;
     return RT_OK;

@@ -147,7 +147,9 @@ typedef struct {
                                   no trace launch)                                          */
     uint64_t trace_launches;   /* trace_kernel launches timed in trace_ms                  */
     double exchange_ms;        /* multi-GPU rt_render: host wall time of the RCCL slice exchange
-                                  and gather (max over devices)                            */
+                                  and gather (max over devices).  The multi-GPU render runs
+                                  without per-bounce events: process_ms, sort_ms and trace_ms
+                                  stay 0 there unless RTAMD_MULTI_EVENTS=1                  */
 } rt_stats;
 
 void rt_default_opts(rt_opts *opts);

@@ -165,15 +165,20 @@ def test_fused_and_plain_reorder_bitexact(gpu, monkeypatch, scene, image, sort, 
     assert gst["hits"] == ost["hits_triangle"] + ost["hits_sphere"] and gst["misses"] == ost["misses"]
 
 
-@pytest.mark.parametrize("scene,image,sort", [("cornell_plus", (40, 32, 350, 5), True),    # 18 passes: two chunks
+@pytest.mark.parametrize("scene,image,sort", [("cornell_plus", (40, 32, 350, 5), True),    # 18 passes: two calls of 16
                                               ("cornell", (33, 17, 190, 4), False),        # 10 passes, odd size
                                               ("teapot", (64, 36, 45, 16), True)])         # short last pass
-@pytest.mark.parametrize("xchg", ["overlap", "overlap1", "sync"])
+@pytest.mark.parametrize("xchg", ["overlap", "overlap-rccl", "overlap1", "sync"])
 def test_multi_device_rccl_bitexact(gpu, monkeypatch, scene, image, sort, xchg):
     """rt_render with rt_opts.device_count (in-library pass sharding over an RCCL communicator,
     slice all-to-all, ordered owner adds, gather to the first device) at N = 1, the only device
     count this box has: bit-exact against the oracle and the single-device render.  The exchange
-    runs overlapped with the render (round 5: every 4 rounds, or every round) or after each chunk."""
+    runs overlapped with the render (round 5: every 4 rounds, or every round) or after each chunk.
+    At N = 1 the all-to-all and the gather are the identity and are skipped; "overlap-rccl", "overlap1" and
+    "sync" run them through RCCL anyway (RTAMD_XCHG_IDENTITY=0)."""
+    if xchg != "overlap":
+        monkeypatch.setenv("RTAMD_XCHG_IDENTITY", "0")
+    monkeypatch.setenv("RTAMD_XCHG_CHUNK", "16")            # more than 16 rounds: two renderer calls
     if xchg == "sync":
         monkeypatch.setenv("RTAMD_XCHG_OVERLAP", "0")
     elif xchg == "overlap1":
@@ -191,7 +196,8 @@ def test_multi_device_rccl_bitexact(gpu, monkeypatch, scene, image, sort, xchg):
     (2, "teapot", (64, 36, 100, 16), True, "overlap"),       # 5 passes: device 1 has no pass in the last round
     (3, "cornell_plus", (40, 32, 350, 5), True, "overlap1"),  # 18 passes, 6 rounds
     (5, "cornell", (33, 17, 190, 4), False, "sync"),          # 10 passes, odd size: padded slices
-    (2, "cornell", (24, 16, 700, 3), True, "overlap"),        # 35 passes = 18 rounds: two chunks of rounds
+    (2, "cornell", (24, 16, 700, 3), True, "overlap"),        # 35 passes = 18 rounds: two calls of 16 rounds
+    (2, "cornell", (24, 16, 700, 3), True, "overlap-1call"),  # the same in one call (the default chunk)
 ])
 def test_multi_device_loopback_bitexact(gpu, monkeypatch, world, scene, image, sort, xchg):
     """The in-library multi-device render at N > 1 on the box's one GPU (round 5): RTAMD_MULTI_LOOPBACK=1 runs
@@ -199,6 +205,8 @@ def test_multi_device_loopback_bitexact(gpu, monkeypatch, world, scene, image, s
     two ranks on one GPU), so the pass dealing, the stale rows of rounds a device has no pass in, the overlapped
     exchange, the owners' ordered adds and the gather all run at N = 2 / 3 / 5: bit-exact against the oracle."""
     monkeypatch.setenv("RTAMD_MULTI_LOOPBACK", "1")
+    if xchg != "overlap-1call":
+        monkeypatch.setenv("RTAMD_XCHG_CHUNK", "16")
     if xchg == "sync":
         monkeypatch.setenv("RTAMD_XCHG_OVERLAP", "0")
     elif xchg == "overlap1":
