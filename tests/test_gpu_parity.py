@@ -165,6 +165,22 @@ def test_fused_and_plain_reorder_bitexact(gpu, monkeypatch, scene, image, sort, 
     assert gst["hits"] == ost["hits_triangle"] + ost["hits_sphere"] and gst["misses"] == ost["misses"]
 
 
+@pytest.mark.parametrize("home", ["0", "1"])
+@pytest.mark.parametrize("scene,image", [("teapot", (96, 54, 40, 16)), ("cornell_plus", (48, 40, 60, 8)),
+                                         ("spheres", (64, 48, 40, 8))])
+def test_home_indexed_radiance_bitexact(gpu, monkeypatch, scene, image, home):
+    """Sort on with the fused bounce-0 reorder (round 5): a surviving ray's radiance lives at its home index (its
+    bounce-1 slot), the replay writes bounce-0 emission there and home_of[ray id] for the accumulation; RTAMD_HOME=0
+    keeps acc[ray id].  cornell_plus has an emitter (radiance terms at bounce 0 and later, the read-modify-write
+    path), spheres runs the fused replay at every bounce; both forms equal the oracle bit for bit."""
+    monkeypatch.setenv("RTAMD_HOME", home)
+    osc, psc = _pair(scene, image)
+    ofb, ost = osc.render(sort=True)
+    gfb, gst = R.render(psc, sort=True)
+    assert np.array_equal(gfb, ofb), _diff(gfb, ofb)
+    assert gst["live_segments"] == ost["live_segments"]
+
+
 @pytest.mark.parametrize("scene,image,sort", [("cornell_plus", (40, 32, 350, 5), True),    # 18 passes: two calls of 16
                                               ("cornell", (33, 17, 190, 4), False),        # 10 passes, odd size
                                               ("teapot", (64, 36, 45, 16), True)])         # short last pass
