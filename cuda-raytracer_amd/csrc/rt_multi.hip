@@ -323,14 +323,17 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
         // adds skip (pass src + N*k does not exist)
         auto t0 = clk::now();
         // RTAMD_TIMING: when the exchange groups ran on the device (events around each group's adds)
-        std::vector<hipEvent_t> gev;
+        struct Events {
+            std::vector<hipEvent_t> v;
+            ~Events() { for (hipEvent_t e : v) (void)hipEventDestroy(e); }
+        } gevs;
+        std::vector<hipEvent_t> &gev = gevs.v;
         const bool gtime = std::getenv("RTAMD_TIMING") != nullptr;
         auto gmark = [&]() -> int {
             if (!gtime) return RT_OK;
-            hipEvent_t e = nullptr;
-            MHIP(hipEventCreate(&e));
-            gev.push_back(e);
-            MHIP(hipEventRecord(e, g.s));
+            gev.push_back(nullptr);
+            MHIP(hipEventCreate(&gev.back()));
+            MHIP(hipEventRecord(gev.back(), g.s));
             return RT_OK;
         };
         if (int rc_ = gmark()) return rc_;
@@ -377,7 +380,6 @@ int run_device(const rt_scene *scene, const rt_opts *base, Link &ln, int world, 
                 MHIP(hipEventElapsedTime(&ms, gev[0], gev[k]));
                 line += (k % 2 ? " ready " : " added ") + std::to_string(ms);
             }
-            for (hipEvent_t e : gev) (void)hipEventDestroy(e);
             std::fprintf(stderr, "rt_multi device %d chunk at round %d: exchange groups (ms after the chunk's enqueue):%s; "
                          "host wait after the render %.2f ms\n", st.rank, k0, line.c_str(),
                          std::chrono::duration<double, std::milli>(clk::now() - tf).count());
