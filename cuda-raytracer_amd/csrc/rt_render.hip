@@ -637,7 +637,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void trace_kernel(DevScene S,
 }
 
 // One ray's shading (scene.cu:376-485) at `slot`: environment lookup on a miss, otherwise
-// emission + scatter.  Returns the new state; `ray` = the ray id (acc index), kind = 0 miss,
+// emission + scatter.  Returns the new state; `ray` = the acc index (ray id or home index), kind = 0 miss,
 // 1 triangle hit, 2 sphere hit.
 struct Shaded {
     V3 no, nd, T;
@@ -1429,9 +1429,9 @@ struct InitTimer {
 struct PassCtx {
     hipStream_t stream = nullptr;
     // Ray state in slot order, ping-ponged by the reorder (sort off: one copy, slot = ray id):
-    // geo = 2 x float4 {o.xyz, d.x} {d.yz, T.xy}, tz = T.z, rid = ray id (+ kAccFlag).  acc[ray id]
-    // holds {T.z, C}: the radiance once a bounce added a nonzero term, and finally when the ray terminates
-    // or after the last bounce.
+    // geo = 2 x float4 {o.xyz, d.x} {d.yz, T.xy}, tz = T.z, rid = the ray's acc index (+ kAccFlag): its ray id,
+    // or its home index (Renderer::home).  acc[that] holds {T.z, C}: the radiance once a bounce added a nonzero
+    // term, and finally when the ray terminates or after the last bounce.
     DevBuf<float4> geo[2], acc;
     DevBuf<float> tz[2];
     DevBuf<uint32_t> rid[2], sort_counts, sort_offsets, sort_totals, live, queue, overflow;
