@@ -5,22 +5,31 @@ Workload (default): teapot.scene at 1920x1080, 2048 spp, 16 bounces, sort on (BA
 configs[3], the config the north star's roofline target is stated on).  A step is one 20-spp
 pass of the hot path on every GPU: ray generation, 16 x (BVH traversal + shading + reorder
 key, stable reorder), ordered accumulation.  Multi-GPU runs shard whole passes round-robin
-over ranks (rank r renders pass r + N*k); the pass framebuffers are exchanged as pixel slices
-(one RCCL all-to-all: rank j owns slice j and adds the slices in pass order, bit-identical to
-1 GPU) and the finished slices are gathered to rank 0.  By default the timed region is one
+over the GPUs (GPU r renders pass r + N*k); the pass framebuffers are exchanged as pixel slices
+(one RCCL all-to-all: GPU j owns slice j and adds the slices in pass order, bit-identical to
+1 GPU) and the finished slices are gathered to GPU 0.  By default the timed region is one
 full frame (strong scaling); `--steps K` times K passes per GPU (weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scene teapot] [--no-sort]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+`--gpus N` is honoured however bench.py is started:
+  * under torchrun (WORLD_SIZE set): one process per GPU, collectives through torch.distributed
+    (RCCL); WORLD_SIZE must equal N, or the run exits with status 2;
+  * without it (WORLD_SIZE unset), N > 1: one process drives the N GPUs through the library's own
+    multi-GPU renderer (rt_multi: ncclCommInitAll over GPUs 0..N-1, one host thread per GPU, the
+    same pass sharding and slice exchange); N above the visible HIP devices exits with status 2.
+Every line carries n_gpus = N and config.n_ranks_seen = the ranks the collective backend counted.
+
 Rank 0 prints ONE JSON line.  `value` = live ray segments (process_ray calls on live slots)
 per second over all GPUs, inputs resident in HBM.  `render_wall_ms` = one full frame (the
 metric's second column); `bit_exact_vs_oracle` = this run's pass-0 framebuffer hashed against
 the oracle's (tests/golden/bench_pass0.json).  `roofline` prices the dominant kernel
-(trace_kernel) per launch: algorithmic HBM bytes and the measured PMC traffic against HBM,
-SURVEY.md §8(d)'s logical cache-inclusive bytes against the L2; `cpu_baseline` times the
-oracle's restatement of the reference `cpu` path on the host cores (§8(d): first pass +
-remainder pass, extrapolated).
+(trace_kernel) inside the timed step (its wave-residency share of a pass x ms_per_step):
+algorithmic HBM bytes and the measured PMC traffic against HBM, with the exclusive-launch
+figures, the per-launch table and SURVEY.md §8(d)'s logical cache-inclusive bytes (against the
+L2) as labelled secondary fields; `cpu_baseline` times the oracle's restatement of the
+reference `cpu` path on the host cores (§8(d): first pass + remainder pass, extrapolated).
 """
 import argparse
 import json
@@ -34,9 +43,25 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 # queues would make them share queues (20 in flight: 24 queues beat 16 by 1.5 % on teapot, 3.4 %
 # on lamp).  With torch.distributed (RCCL) in the process its streams need queues too (16 passes
 # and 16 queues cost the 1-GPU --dist run 11 %).  Set before HIP initialises.
-_DIST = int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dist" in sys.argv
-_QUEUES = int(os.environ.get("RTAMD_HW_QUEUES", "0") or 0) or (28 if _DIST else 24)   # RTAMD_HW_QUEUES: sweeps only
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _QUEUES or "RTAMD_HW_QUEUES" in os.environ:
+def _argv_gpus(argv):
+    """--gpus N from the command line before argparse runs (the queue count must be set before HIP starts)."""
+    for i, a in enumerate(argv):
+        try:
+            if a == "--gpus" and i + 1 < len(argv):
+                return int(argv[i + 1])
+            if a.startswith("--gpus="):
+                return int(a.split("=", 1)[1])
+        except ValueError:
+            return 1
+    return 1
+
+
+_DIST = int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dist" in sys.argv or _argv_gpus(sys.argv) > 1
+_HWQ = os.environ.get("RTAMD_HW_QUEUES")            # RTAMD_HW_QUEUES: sweeps only
+if _HWQ is not None and not (_HWQ.isdigit() and 1 <= int(_HWQ) <= 32):
+    sys.exit("bench.py: RTAMD_HW_QUEUES=%r: expected a queue count in 1..32" % _HWQ)
+_QUEUES = int(_HWQ) if _HWQ else (28 if _DIST else 24)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _QUEUES or _HWQ:
     os.environ["GPU_MAX_HW_QUEUES"] = str(_QUEUES)
 # Next to RCCL, 16 passes in flight beat 20 (1-GPU --dist: 7.63 vs 7.76 ms/pass for a frame, 8.10
 # vs 9.0-12.7 for a 13-pass share); alone, 20 are faster.
@@ -193,42 +218,68 @@ def cpu_baseline(cfg, args):
 
 
 def roofline(excl, counted, launches, trace_ms, scene_bytes, spheres, workload, elapsed, steps):
-    """The dominant kernel (trace_kernel) against HBM, per launch, reproducible from committed files:
-    achieved = algorithmic bytes / exclusive launch duration; traffic = rocprofv3 --pmc fabric bytes
-    of the same serialised pass (profiles/pmc_traffic.json, with the profiler's own per-launch
-    durations beside them).  The timed region's shared-chip spans are a labelled secondary field."""
+    """The dominant kernel (trace_kernel) against HBM, reproducible from committed files.  Headline (round 6):
+    the kernel inside the timed step (timed_regime: its wave-residency share of a pass x ms_per_step, so its
+    time never exceeds the step): achieved = one pass's algorithmic trace bytes / that time, traffic = the
+    PMC fabric bytes of one pass's trace launches (profiles/pmc_traffic.json) over the same time.  Secondary,
+    labelled: `exclusive` (pass 0 alone on the chip, per launch; 16 such launches take longer than a timed
+    step, so they describe another regime), `shared` (the timed steps' launch spans, which overlap), the
+    per-launch table, the L2 and VALU figures."""
     xc = excl["counted"]
     n_ex = excl["launches"]
     ms_ex = excl["ms_per_launch"]
     comp_ex = compulsory_trace_bytes(xc, scene_bytes, n_ex, per_xcd=True) / n_ex
     logical_ex = logical_trace_bytes(xc, spheres) / n_ex
-    achieved = comp_ex / (ms_ex / 1e3) / 1e9
+    achieved_ex = comp_ex / (ms_ex / 1e3) / 1e9
     pmc = load_pmc(workload)
-    traffic = pmc["trace_bytes_per_launch"] if pmc else None
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "trace_kernel (BVH traversal + Moller-Trumbore + slab + sphere loop), per launch",
-            "bytes_per_launch": int(comp_ex), "ms_per_launch": round(ms_ex, 4), "launches": n_ex,
-            "exclusive_pass_kernel_ms": round(excl["kernel_ms"], 3),
-            "achieved_def": "algorithmic HBM bytes per trace launch of pass 0 run alone on the chip (24 B ray read "
-                            "per live segment past bounce 0 + 8 B hit write per live segment + the scene's node and "
-                            "triangle arrays (reference layouts, 32 / 48 B) once per XCD: 8 non-coherent 4 MB L2s each "
-                            "fetch the scene) / its exclusive average launch duration (device wall clock, first wave "
-                            "start to last wave end, one pass context, trace grid = every resident workgroup, best "
-                            "of 3, measured before the warmup; bench.py exclusive_pass)",
-            "traffic_def": None if not pmc else
-            "measured fabric-side bytes per trace launch, rocprofv3 --pmc over exactly pass 0 with dispatches "
-            "serialised (%s; reads priced by request size TCC_EA0_RDREQ_{128B,64B,32B}, = 2 x FETCH_SIZE for 128-B "
-            "requests per MI355X_MICROARCH.md §HBM; writes TCC_EA0_WRREQ{,_64B}; Infinity-Cache hits included, "
-            "an upper bound on HBM bytes); %s" % (pmc["file"], pmc.get("run", "")),
-            "traffic_frac": round(traffic / (ms_ex / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
-            "traffic_over_algorithmic": round(traffic / comp_ex, 3) if traffic else None}
+    traffic_ex = pmc["trace_bytes_per_launch"] if pmc else None
+    kernel = "trace_kernel (BVH traversal + Moller-Trumbore + slab + sphere loop)"
+    exclusive = {
+        "achieved": round(achieved_ex, 1), "frac": round(achieved_ex / HBM_PEAK_GBS, 4), "traffic": traffic_ex,
+        "bytes_per_launch": int(comp_ex), "ms_per_launch": round(ms_ex, 4), "launches": n_ex,
+        "exclusive_pass_kernel_ms": round(excl["kernel_ms"], 3),
+        "achieved_def": "secondary, another regime than the timed step: algorithmic HBM bytes per trace launch of "
+                        "pass 0 run alone on the chip (24 B ray read per live segment past bounce 0 + 8 B hit write "
+                        "per live segment + the scene's node and triangle arrays (reference layouts, 32 / 48 B) "
+                        "once per XCD: 8 non-coherent 4 MB L2s each fetch the scene) / its exclusive average launch "
+                        "duration (device wall clock, first wave start to last wave end, one pass context, trace "
+                        "grid = every resident workgroup, best of 3, measured before the warmup; bench.py "
+                        "exclusive_pass)",
+        "traffic_def": None if not pmc else
+        "measured fabric-side bytes per trace launch, rocprofv3 --pmc over exactly pass 0 with dispatches "
+        "serialised (%s; reads priced by request size TCC_EA0_RDREQ_{128B,64B,32B}, = 2 x FETCH_SIZE for 128-B "
+        "requests per MI355X_MICROARCH.md §HBM; writes TCC_EA0_WRREQ{,_64B}; Infinity-Cache hits included, "
+        "an upper bound on HBM bytes); %s" % (pmc["file"], pmc.get("run", "")),
+        "traffic_frac": round(traffic_ex / (ms_ex / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic_ex else None,
+        "traffic_over_algorithmic": round(traffic_ex / comp_ex, 3) if traffic_ex else None}
     if pmc and pmc.get("trace_dur_ms_avg"):
-        roof["pmc_run"] = {"ms_per_launch": round(pmc["trace_dur_ms_avg"], 4),
-                           "fabric_gbs": round(pmc["trace_fabric_gbs"], 1),
-                           "frac": round(pmc["trace_fabric_gbs"] / HBM_PEAK_GBS, 4),
-                           "def": "the PMC run's own numbers: fabric bytes per trace launch / the profiler's average "
-                                  "trace dispatch duration (profiles/pmc_traffic.json trace_dur_ms_per_launch)"}
+        exclusive["pmc_run"] = {"ms_per_launch": round(pmc["trace_dur_ms_avg"], 4),
+                                "fabric_gbs": round(pmc["trace_fabric_gbs"], 1),
+                                "frac": round(pmc["trace_fabric_gbs"] / HBM_PEAK_GBS, 4),
+                                "def": "the PMC run's own numbers: fabric bytes per trace launch / the profiler's "
+                                       "average trace dispatch duration (profiles/pmc_traffic.json "
+                                       "trace_dur_ms_per_launch)"}
+    iss = load_issue(workload)
+    timed = timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps)
+    if timed:
+        roof = {"bound": "hbm", "achieved": timed["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": timed["frac"], "traffic": timed.get("measured_bytes_per_step"),
+                "traffic_frac": timed.get("measured_frac"), "regime": "timed step",
+                "kernel": kernel + ", inside the timed step",
+                "bytes_per_step": timed["algorithmic_bytes_per_step"], "kernel_ms_per_step": timed["ms_per_step"],
+                "traffic_unit": "bytes per step (the trace launches of one pass, rocprofv3 --pmc)",
+                "achieved_def": "one pass's algorithmic trace bytes (24 B ray read per live segment past bounce 0 + "
+                                "8 B hit write per live segment + the scene once per XCD per launch) / the trace "
+                                "kernel's time per step (its SQ_WAVE_CYCLES share of one pass x ms_per_step, "
+                                "roofline.timed); traffic = the PMC fabric bytes of one pass's trace launches over "
+                                "the same time (traffic_frac)"}
+    else:
+        roof = {"bound": "hbm", "achieved": exclusive["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": exclusive["frac"], "traffic": traffic_ex, "traffic_frac": exclusive["traffic_frac"],
+                "regime": "exclusive launch (no committed PMC issue record for this workload)",
+                "kernel": kernel + ", per exclusive launch", "bytes_per_launch": int(comp_ex),
+                "ms_per_launch": round(ms_ex, 4), "achieved_def": exclusive["achieved_def"]}
+    roof["exclusive"] = exclusive
     comp_sh = compulsory_trace_bytes(counted, scene_bytes, launches, per_xcd=True) / launches
     roof["shared"] = {"ms_per_launch": round(trace_ms, 4), "launches": launches,
                       "achieved": round(comp_sh / (trace_ms / 1e3) / 1e9, 1),
@@ -259,8 +310,6 @@ def roofline(excl, counted, launches, trace_ms, scene_bytes, spheres, workload, 
     table = per_launch_table(excl, scene_bytes, pmc)
     if table:
         roof.update(table)
-    iss = load_issue(workload)
-    timed = timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps)
     if timed:
         roof["timed"] = timed
     if iss and steps:
@@ -274,8 +323,6 @@ def roofline(excl, counted, launches, trace_ms, scene_bytes, spheres, workload, 
                                "profiles/pmc_issue.json: %s) / timed wall per pass, against the chip's issue "
                                "rate (1024 SIMD-32 x 2.4 GHz / 2 cycles)" % iss.get("run", "")}
     return roof
-
-
 
 
 def timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps):
@@ -466,9 +513,45 @@ class RtamdBackend:
             self.dist.destroy_process_group()
 
 
+class InLibBackend(RtamdBackend):
+    """--gpus N without torchrun: one process drives N GPUs through the library's own multi-GPU renderer
+    (rt_multi: one RCCL communicator from ncclCommInitAll, one host thread and renderer per GPU, the pass
+    sharding and overlapped slice exchange of rt_render's device_count path).  The frame is
+    gathered on GPU 0; the stats are summed over the GPUs.  With the test build (RTAMD_LIB =
+    librtamd_test.so) and RTAMD_MULTI_LOOPBACK=1 the N "GPUs" are the box's one GPU (tests only)."""
+    inlib = True
+
+    def __init__(self, n):
+        self.world, self.rank, self.local = n, 0, 0
+        self.dist = self.torch = self.device = None
+        self.use_dist = False
+        self.probe = None
+        loopback = os.environ.get("RTAMD_MULTI_LOOPBACK") == "1" and rtamd.LIB_PATH == rtamd.TEST_LIB_PATH
+        visible = rtamd.device_count()
+        if not loopback and n > visible:
+            raise SystemExit2("bench.py: --gpus %d but %d HIP device(s) visible" % (n, visible))
+        self.devices = [0] * n if loopback else list(range(n))
+        self.loopback = loopback
+
+    def renderer(self, scene, sort, tiles):
+        if tiles:
+            raise SystemExit2("bench.py: --shard tiles / --tile-share need one process per GPU (torchrun)")
+        return rtamd.MultiRenderer(scene, self.devices, sort=sort)
+
+
+class SystemExit2(SystemExit):
+    """A usage error that ends the run with exit status 2 (message on stderr)."""
+
+    def __init__(self, msg):
+        print(msg, file=sys.stderr)
+        super().__init__(2)
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (default: WORLD_SIZE under torchrun, else 1); without torchrun N > 1 runs the "
+                         "library's in-process multi-GPU renderer")
     ap.add_argument("--steps", type=int, default=None,
                     help="passes per GPU to time (default: one full frame, ceil(passes/N) per GPU)")
     ap.add_argument("--warmup", type=int, default=4)
@@ -499,6 +582,7 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
     world, rank = backend.world, backend.rank
     dist, torch = backend.dist, backend.torch
     use_dist = dist is not None
+    inlib = getattr(backend, "inlib", False)     # one process, N GPUs through rt_multi
     name = args.scene
     cfg = cfg or CONFIGS[name]
     scene_file, W, H, spp, bounces, sort, use_bvh = cfg
@@ -577,6 +661,12 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
                 frame.reset()
                 mine += frame.run_rounds(0, m)
                 frame.collect()
+            elif inlib:
+                # the first m rounds of the frame over the N GPUs in one library call (rt_multi_run: pass
+                # p on GPU p mod N, the slice exchange overlapped, the frame gathered on GPU 0)
+                n = min(P, world * m)
+                accumulate_stats(ren.run(pass_count=n))
+                mine += n
             else:
                 accumulate_stats(ren.run(pass_begin=0, count=m, stride=1))
                 mine += m
@@ -604,6 +694,9 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
     warm = {}
     run_steps(args.warmup, warm)
     backend.barrier_sync()
+    single = not use_dist and not inlib and not tiles
+    if single and full_frame:
+        ren.clear()                     # the renderer's framebuffer then holds exactly the timed frame
     timed = {}
     t0 = time.perf_counter()
     my_passes = run_steps(steps, timed)
@@ -612,6 +705,8 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
     timed_fb = None
     if use_dist and rank == 0 and frame.fb is not None:
         timed_fb = frame.fb.detach().to("cpu").numpy().copy()
+    elif (inlib or single) and full_frame and rank == 0:
+        timed_fb = ren.framebuffer()
 
     # ---- untimed legs (every rank takes part: they contain collectives)
     evrun, counted, frame_s, parity = {}, None, None, None
@@ -650,13 +745,15 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
                       "sha256_pass0": digest,
                       "oracle": "tests/golden/bench_pass0.json (CPU oracle, tests/golden/make_bench_hashes.py)"
                       if gold else "no golden hash for this workload",
+                      **frame_parity(timed_fb, name, sort, (W, H, spp, bounces) if full_frame and frame_spp == spp
+                                     else None),
                       "reference_rms": "parity unpinned: the reference's GPU path cannot run here (SURVEY.md §8c), "
                                        "the oracle is a cited restatement; image error vs the reference is not "
                                        "measured (DESIGN.md: the fast-math floor)"}
     elapsed, frame_s_max = reduce([elapsed, frame_s or 0.0], "max")
     # ranks that took part, as the collective backend counts them (a SCALE run can be checked for
-    # RCCL seeing N ranks): an all-reduce of 1 per rank
-    n_ranks_seen = int(reduce([1.0])[0])
+    # RCCL seeing N ranks): an all-reduce of 1 per rank (in-library: per GPU, done by rt_multi_create)
+    n_ranks_seen = ren.ranks if inlib else int(reduce([1.0])[0])
     live, gen = reduce([timed.get("live_segments", 0), timed.get("generated_rays", 0)])
 
     out = None
@@ -668,7 +765,14 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
         trace_ms = evrun.get("trace_ms", 0.0) / launches if launches else 0.0
         roof = None
         if counted and launches and trace_ms > 0 and excl:
-            roof = roofline(excl, counted, launches, trace_ms, scene_bytes, v.sphere_count, workload, elapsed, steps)
+            pg_counted, pg_launches = counted, launches
+            if inlib and world > 1:
+                # the counters and launches are summed over the N GPUs: one GPU's share per step (passes cost
+                # the same), as the per-process path reports rank 0's own
+                pg_counted = {k: v // world for k, v in counted.items()}
+                pg_launches = max(1, launches // world)
+            roof = roofline(excl, pg_counted, pg_launches, trace_ms, scene_bytes, v.sphere_count, workload, elapsed,
+                            steps)
         value = live / elapsed / 1e6 if elapsed > 0 else 0.0
         nominal = gen * bounces / elapsed / 1e6 if elapsed > 0 else 0.0
         ms_step = elapsed / steps * 1e3 if steps else 0.0
@@ -695,6 +799,10 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
                 "timed": ("one full frame (%d passes)" % P) if full_frame else ("%d passes per GPU" % steps),
                 "parallelism": ("pixel-tile x%d (%d-row stripes) + RCCL gather" % (world, TILE_ROWS) if tiles else
                                 "pass-shard x%d + RCCL all-to-all/gather" % world) if world > 1 else "single GPU",
+                "launch": ("one process, %d GPUs through the library's rt_multi (ncclCommInitAll)%s"
+                           % (world, ", loopback test transport on one GPU" if getattr(backend, "loopback", False)
+                              else "")) if inlib else ("one process per GPU (torch.distributed over RCCL)"
+                                                       if use_dist else "one process"),
                 "nominal_mrays_per_s": round(nominal, 2),
                 "render_wall_def": "one full frame (%d passes), first pass to the accumulated framebuffer on the "
                                    "GPU, inputs resident (%s)" % (-(-spp // 20), "the timed region" if full_frame else
@@ -745,6 +853,43 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
     return {"line": out, "timed_fb": timed_fb, "my_passes": my_passes, "frame_passes": P} if rank == 0 else None
 
 
+def frame_parity(fb, name, sort, image):
+    """The timed region's whole frame (when it is the configured frame) hashed against the oracle's
+    (tests/golden/bench_frames.json: cornell, cornell_plus, spheres)."""
+    if fb is None or image is None:
+        return {}
+    try:
+        with open(os.path.join(REPO, "tests", "golden", "bench_frames.json")) as f:
+            gold = json.load(f).get("%s frame sort=%s" % (name, "on" if sort else "off"))
+    except (OSError, ValueError):
+        gold = None
+    if not gold or list(gold["image"]) != list(image):
+        return {}
+    import hashlib
+    digest = hashlib.sha256(np.asarray(fb, dtype="<f4").tobytes()).hexdigest()
+    return {"frame_bit_exact_vs_oracle": digest == gold["sha256"], "sha256_frame": digest,
+            "frame_oracle": "tests/golden/bench_frames.json (the timed frame, assembled over the GPUs)"}
+
+
+def make_backend(args):
+    """The backend `--gpus N` asks for (see the module docstring); exits with status 2 on a mismatch."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        world = int(ws)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit2("bench.py: --gpus %d but WORLD_SIZE=%d (torchrun --nproc-per-node must equal --gpus)"
+                              % (args.gpus, world))
+        return RtamdBackend(use_dist=world > 1 or args.dist)
+    n = args.gpus if args.gpus is not None else 1
+    if n < 1:
+        raise SystemExit2("bench.py: --gpus must be at least 1")
+    if n > 1:
+        if args.dist:
+            raise SystemExit2("bench.py: --dist with --gpus > 1 needs torchrun (one process per GPU)")
+        return InLibBackend(n)
+    return RtamdBackend(use_dist=args.dist)
+
+
 def main():
     args = parse_args()
     # The JSON line is the only thing on stdout: native libraries (RCCL prints a version banner)
@@ -752,8 +897,7 @@ def main():
     json_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    backend = RtamdBackend(use_dist=world > 1 or args.dist)
+    backend = make_backend(args)
     import make_envmap
     make_envmap.ensure_envmap(os.path.join(REPO, "assets", "teapot", "textures", "envmap.pfm"))
     run(args, backend, json_out=json_out)

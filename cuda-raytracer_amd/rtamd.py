@@ -13,11 +13,14 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 BUILD_DIR = os.path.join(PKG_DIR, "build")
-# Up to 20 passes in flight on their own streams: ask HIP for enough hardware queues (effective
-# only if HIP has not initialised in this process yet).
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
-    os.environ["GPU_MAX_HW_QUEUES"] = "24"
+# Up to 20 passes in flight on their own streams: HIP needs a hardware queue per stream.  Loading
+# librtamd.so asks for 24 unless the variable is set (rt_abi.h); setting the same default here also
+# covers a process where torch initialises HIP before the library loads.  A caller's value stands.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "24")
 LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(BUILD_DIR, "librtamd.so")  # env: A/B builds only
+# the same library with the multi-GPU test hooks (one-GPU loopback transport, failure injection):
+# tests only, loaded beside the product library (test_lib())
+TEST_LIB_PATH = os.path.join(BUILD_DIR, "librtamd_test.so")
 CLI_PATH = os.path.join(BUILD_DIR, "raytracing")
 HEADER = os.path.join(REPO, "include", "rt_abi.h")
 ASSETS = os.path.join(REPO, "assets")
@@ -86,46 +89,69 @@ def build(jobs=8):
     subprocess.run(["make", "-s", "-j%d" % jobs, "-C", PKG_DIR], check=True)
 
 
+_test_lib = None
+
+
 def lib():
     """Load librtamd.so.  Raises if it has not been built: no fallback exists."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RtError("librtamd.so is not built (run `make -C cuda-raytracer_amd` or "
-                          "__graft_entry__.build())")
-        L = C.CDLL(LIB_PATH)
-        L.rt_last_error.restype = C.c_char_p
-        L.rt_abi_version.restype = C.c_int
-        L.rt_device_count.restype = C.c_int
-        L.rt_default_opts.argtypes = [P]
-        L.rt_default_load_opts.argtypes = [P]
-        L.rt_scene_load.argtypes = [C.c_char_p, P, C.POINTER(P)]
-        L.rt_scene_view.argtypes = [P]
-        L.rt_scene_view.restype = C.POINTER(RtScene)
-        L.rt_scene_bvh_ms.argtypes = [P]
-        L.rt_scene_bvh_ms.restype = C.c_double
-        L.rt_scene_free.argtypes = [P]
-        L.rt_render.argtypes = [P, P, P, P]
-        L.rt_renderer_create.argtypes = [P, P, C.POINTER(P)]
-        L.rt_renderer_run.argtypes = [P, I32, I32, I32, P, P]
-        L.rt_renderer_run_host.argtypes = [P, I32, I32, I32, P, P]
-        L.rt_renderer_read_framebuffer.argtypes = [P, P]
-        L.rt_renderer_clear.argtypes = [P]
-        L.rt_renderer_set_counters.argtypes = [P, I32]
-        L.rt_renderer_destroy.argtypes = [P]
-        L.rt_trace_rays.argtypes = [P, P, P, I32, P, P, P]
-        L.rt_bloom.argtypes = [P, I32, I32, C.c_float, I32, I32]
-        L.rt_bloom_device.argtypes = [P, I32, I32, C.c_float, I32, I32]
-        L.rt_tonemap.argtypes = [P, I32, I32, C.c_float, I32, P]
-        L.rt_write_png.argtypes = [C.c_char_p, P, I32, I32]
-        L.rt_cpu_render.argtypes = [P, P, I32, C.POINTER(C.c_double)]
-        _lib = L
+        _lib = _load(LIB_PATH)
     return _lib
 
 
-def _check(rc):
+def test_lib():
+    """librtamd_test.so (the test-hook build: RTAMD_MULTI_LOOPBACK, RTAMD_FAIL_AFTER_SETUP), for tests.
+    Scenes loaded through lib() can be passed to it: rt_scene is a plain host view."""
+    global _test_lib
+    if _test_lib is None:
+        _test_lib = _load(TEST_LIB_PATH)
+    return _test_lib
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise RtError("%s is not built (run `make -C cuda-raytracer_amd` or "
+                      "__graft_entry__.build())" % os.path.basename(path))
+    L = C.CDLL(path)
+    L.rt_last_error.restype = C.c_char_p
+    L.rt_abi_version.restype = C.c_int
+    L.rt_device_count.restype = C.c_int
+    L.rt_default_opts.argtypes = [P]
+    L.rt_default_load_opts.argtypes = [P]
+    L.rt_scene_load.argtypes = [C.c_char_p, P, C.POINTER(P)]
+    L.rt_scene_view.argtypes = [P]
+    L.rt_scene_view.restype = C.POINTER(RtScene)
+    L.rt_scene_bvh_ms.argtypes = [P]
+    L.rt_scene_bvh_ms.restype = C.c_double
+    L.rt_scene_free.argtypes = [P]
+    L.rt_render.argtypes = [P, P, P, P]
+    L.rt_renderer_create.argtypes = [P, P, C.POINTER(P)]
+    L.rt_renderer_run.argtypes = [P, I32, I32, I32, P, P]
+    L.rt_renderer_run_host.argtypes = [P, I32, I32, I32, P, P]
+    L.rt_renderer_read_framebuffer.argtypes = [P, P]
+    L.rt_renderer_clear.argtypes = [P]
+    L.rt_renderer_set_counters.argtypes = [P, I32]
+    L.rt_renderer_destroy.argtypes = [P]
+    L.rt_trace_rays.argtypes = [P, P, P, I32, P, P, P]
+    L.rt_bloom.argtypes = [P, I32, I32, C.c_float, I32, I32]
+    L.rt_bloom_device.argtypes = [P, I32, I32, C.c_float, I32, I32]
+    L.rt_tonemap.argtypes = [P, I32, I32, C.c_float, I32, P]
+    L.rt_write_png.argtypes = [C.c_char_p, P, I32, I32]
+    L.rt_cpu_render.argtypes = [P, P, I32, C.POINTER(C.c_double)]
+    L.rt_multi_create.argtypes = [P, P, C.POINTER(P)]
+    L.rt_multi_run.argtypes = [P, I32, P, P]
+    L.rt_multi_read_framebuffer.argtypes = [P, P]
+    L.rt_multi_set_event_timing.argtypes = [P, I32]
+    L.rt_multi_set_counters.argtypes = [P, I32]
+    L.rt_multi_ranks.argtypes = [P]
+    L.rt_multi_destroy.argtypes = [P]
+    return L
+
+
+def _check(rc, L=None):
     if rc != 0:
-        raise RtError("rt error %d: %s" % (rc, lib().rt_last_error().decode()))
+        raise RtError("rt error %d: %s" % (rc, (L or lib()).rt_last_error().decode()))
 
 
 def _ptr(a):
@@ -242,10 +268,12 @@ def tile_rows_of(height, tile_count, tile_index, tile_rows=8):
 
 
 def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=1, counters=False,
-           tiles=None, devices=None, shard_tiles=False):
+           tiles=None, devices=None, shard_tiles=False, L=None):
     """rt_render: the drop-in for gpu_raytrace.  Returns (framebuffer W*H*3 float32, stats).
     devices = list of device ordinals: the in-library multi-GPU render (pass sharding + RCCL
-    slice exchange and gather; rt_opts.device_count/device_ids), also at one device."""
+    slice exchange and gather; rt_opts.device_count/device_ids), also at one device.
+    L = the library to call (default lib(); tests: test_lib())."""
+    L = L or lib()
     fb = np.zeros(scene.pixels * 3, np.float32)
     st = RtStats()
     o = default_opts(sort, device, pass_begin, pass_count, pass_stride, counters, tiles)
@@ -255,8 +283,56 @@ def render(scene, sort=True, device=0, pass_begin=0, pass_count=-1, pass_stride=
         o.device_count = len(devices)
         o.device_ids = C.cast(ids, C.POINTER(I32))
         o.shard_tiles = int(shard_tiles)
-    _check(lib().rt_render(scene.ptr, C.byref(o), _ptr(fb), C.byref(st)))
+    _check(L.rt_render(scene.ptr, C.byref(o), _ptr(fb), C.byref(st)), L)
     return fb, st.as_dict()
+
+
+class MultiRenderer:
+    """rt_multi: the persistent in-library multi-GPU renderer (one process, one RCCL communicator over
+    `devices`, pass sharding with the slice exchange; the frame is gathered on devices[0])."""
+
+    def __init__(self, scene, devices, sort=True, counters=False, L=None):
+        self.L = L or lib()
+        self.scene = scene
+        o = default_opts(sort, int(devices[0]) if devices else 0, counters=counters)
+        self._ids = (I32 * len(devices))(*[int(d) for d in devices])
+        o.device_count = len(devices)
+        o.device_ids = C.cast(self._ids, C.POINTER(I32))
+        h = P()
+        _check(self.L.rt_multi_create(scene.ptr, C.byref(o), C.byref(h)), self.L)
+        self.h = h
+        self.devices = len(devices)
+
+    def run(self, pass_count=-1, host=False):
+        """Renders passes 0..pass_count-1 of the frame over the devices; returns stats (and the frame
+        when host=True: (fb, stats))."""
+        st = RtStats()
+        fb = np.zeros(self.scene.pixels * 3, np.float32) if host else None
+        _check(self.L.rt_multi_run(self.h, int(pass_count), _ptr(fb) if host else None, C.byref(st)), self.L)
+        return (fb, st.as_dict()) if host else st.as_dict()
+
+    def framebuffer(self):
+        fb = np.zeros(self.scene.pixels * 3, np.float32)
+        _check(self.L.rt_multi_read_framebuffer(self.h, _ptr(fb)), self.L)
+        return fb
+
+    @property
+    def ranks(self):
+        return self.L.rt_multi_ranks(self.h)
+
+    def set_event_timing(self, on):
+        _check(self.L.rt_multi_set_event_timing(self.h, int(on)), self.L)
+
+    def set_counters(self, on):
+        _check(self.L.rt_multi_set_counters(self.h, int(on)), self.L)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.rt_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
 
 RCCL_ID_BYTES = 128   # RT_RCCL_ID_BYTES

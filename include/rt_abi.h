@@ -13,6 +13,9 @@
  * Errors: every int-returning call returns 0 on success or a negative RT_E_* code and
  * records a message readable with rt_last_error() (thread-local).  The reference printed
  * "Error <expr> <msg>" and exit(1) instead (common.cuh:10-18); the CLI keeps that.
+ * Hardware queues: loading the library sets GPU_MAX_HW_QUEUES=24 unless the host has set it (HIP
+ * reads it at initialisation; 4 by default), and a renderer keeps at most that many passes in flight,
+ * one stream each (up to 20).
  * Threading: calls are blocking.  One rt_renderer is bound to one device and must not be
  * used from two threads at once; distinct renderers may run concurrently.
  */
@@ -26,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 enum {
     RT_OK = 0,
@@ -146,6 +149,8 @@ typedef struct {
                                   (event timing on; 0 for scenes without triangles, which have
                                   no trace launch)                                          */
     uint64_t trace_launches;   /* trace_kernel launches timed in trace_ms                  */
+    /* rt_render runs without per-bounce events (like the benchmark's timed passes): its process_ms,
+       sort_ms and trace_ms stay 0 unless RTAMD_EVENTS=1; rt_renderer_run has them by default */
     double exchange_ms;        /* multi-GPU rt_render: host wall time of the RCCL slice exchange
                                   and gather (max over devices).  The multi-GPU render runs
                                   without per-bounce events: process_ms, sort_ms and trace_ms
@@ -236,6 +241,30 @@ int rt_renderer_set_event_timing(rt_renderer *r, int32_t enable);
  * Measurement only; no reference counterpart. */
 int rt_renderer_launch_profile(rt_renderer *r, int32_t cap, double *trace_ms_out, uint32_t *live_out);
 void rt_renderer_destroy(rt_renderer *r);
+
+/* Persistent multi-GPU renderer (one process): rt_render's device_count >= 1 pass sharding
+ * with its set-up kept between renders -- one RCCL communicator over device_ids[0..device_count)
+ * (ncclCommInitAll; NULL = devices 0..device_count-1), one renderer per device (scene resident, 16
+ * passes in flight each) and the slice-exchange buffers.  opts as for rt_render (sort,
+ * collect_counters, device_count, device_ids; pass sharding only: shard_tiles and tile_count are
+ * refused).  rt_multi_create fails with RT_E_NODEVICE when a listed device does not exist, and checks
+ * that every communicator rank answers (an all-reduce of one int per device; rt_multi_ranks returns the
+ * count).  rt_multi_run renders passes 0..pass_count-1 of the frame (-1 = all) round-robin over the
+ * devices (pass p on device p mod N), exchanges the pass sums as pixel slices while later passes
+ * render (ncclAllToAll; each owner adds its slice in pass order, so the image is bit-identical to one
+ * device's) and gathers the frame on device_ids[0]; fb_out (host, W*H*3 floats) receives it unless
+ * NULL, and rt_multi_read_framebuffer copies the last run's frame later.  A run that fails after its
+ * devices started leaves the object unusable (its communicators may be aborted): destroy it.
+ * Blocking; one call at a time per object.  No reference counterpart: the reference ran one device
+ * and allocated per call (raytracing.cu:170-284). */
+typedef struct rt_multi rt_multi;
+int rt_multi_create(const rt_scene *scene, const rt_opts *opts, rt_multi **out);
+int rt_multi_run(rt_multi *m, int32_t pass_count, float *fb_out, rt_stats *stats);
+int rt_multi_read_framebuffer(rt_multi *m, float *fb_out);
+int rt_multi_set_event_timing(rt_multi *m, int32_t enable);   /* per-bounce events (default off) */
+int rt_multi_set_counters(rt_multi *m, int32_t enable);       /* traversal counters (Pn/Iv/Tt)   */
+int rt_multi_ranks(const rt_multi *m);
+void rt_multi_destroy(rt_multi *m);
 
 /* Closest hit of n caller rays: rays = n x {o.x o.y o.z d.x d.y d.z} (d unit length, as every
  * ray the render traces).  The sphere loop (scene.cu:338-372) then bvh_closest_hit_distance

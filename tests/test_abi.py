@@ -43,7 +43,7 @@ def test_struct_layouts():
     assert C.sizeof(R.RtOpts) == 56   # + tile_count/index/rows, device_count, device_ids*, shard_tiles
     assert C.sizeof(R.RtLoadOpts) == 48
     assert C.sizeof(R.RtStats) == 11 * 8 + 8 + 5 * 8 + 8 + 8
-    assert R.lib().rt_abi_version() == 6
+    assert R.lib().rt_abi_version() == 7
 
 
 def test_default_options():
@@ -70,3 +70,27 @@ def test_invalid_arguments_fail_loudly():
     assert b"null" in lib.rt_last_error()
     assert lib.rt_renderer_run(None, 0, 1, 1, None, None) < 0
     assert lib.rt_write_png(b"/nonexistent/x.png", None, 1, 1) < 0
+
+
+def test_test_hooks_only_in_the_test_build():
+    """The one-GPU loopback transport and the failure injection are compiled into librtamd_test.so only
+    (-DRTAMD_TEST_HOOKS): no environment variable can switch the product library's collectives."""
+    for var in (b"RTAMD_MULTI_LOOPBACK", b"RTAMD_FAIL_AFTER_SETUP"):
+        assert var not in open(R.LIB_PATH, "rb").read()
+        assert var in open(R.TEST_LIB_PATH, "rb").read()
+    assert R.test_lib().rt_abi_version() == R.lib().rt_abi_version()
+
+
+def test_library_sets_the_hardware_queue_default():
+    """Loading librtamd.so asks HIP for 24 hardware queues unless the host set GPU_MAX_HW_QUEUES (a
+    constructor that runs before the host's first HIP call), and keeps a host's own value."""
+    code = ("import ctypes, sys; ctypes.CDLL(sys.argv[1]); libc = ctypes.CDLL(None); "
+            "libc.getenv.restype = ctypes.c_char_p; print(libc.getenv(b'GPU_MAX_HW_QUEUES').decode())")
+    env = {k: v for k, v in __import__("os").environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    out = subprocess.run([__import__("sys").executable, "-c", code, R.LIB_PATH], env=env, capture_output=True,
+                         text=True, check=True).stdout.split()
+    assert out == ["24"]
+    env["GPU_MAX_HW_QUEUES"] = "6"
+    out = subprocess.run([__import__("sys").executable, "-c", code, R.LIB_PATH], env=env, capture_output=True,
+                         text=True, check=True).stdout.split()
+    assert out == ["6"]

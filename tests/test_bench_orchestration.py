@@ -158,3 +158,103 @@ def test_bench_run_over_gloo(tmp_path, world, steps):
     ref, _ = O.OracleScene(os.path.join(O.ASSETS, CFG[0]), image=(W, H, frame_spp, bounces)).render(sort=True,
                                                                                                    threads=2)
     assert np.array_equal(got, ref)
+
+
+class OracleMulti:
+    """rtamd.MultiRenderer's interface over the oracle (the in-library backend without torchrun): run(n)
+    renders passes 0..n-1 of the frame, dealt round-robin over the `devices`, each device adding its passes'
+    sums into its own slice of the frame in pass order as rt_multi's owners do -- here every pass is
+    rendered alone and added in pass order, which is that per-pixel sequence."""
+
+    def __init__(self, sc, sort, devices):
+        self.sc, self.sort, self.devices = sc, sort, devices
+        self.fb = None
+        self.ranks = devices
+
+    def run(self, pass_count=-1):
+        P = self.sc.passes if hasattr(self.sc, "passes") else None
+        n = pass_count if pass_count >= 0 else P
+        fb = np.zeros(self.sc.pixels * 3, np.float32)
+        acc = {}
+        for p in range(n):
+            pf, st = self.sc.render(sort=self.sort, pass_begin=p, pass_count=1, threads=2)
+            fb = fb + pf
+            st["hits"] = st["hits_triangle"] + st["hits_sphere"]
+            for k, v in st.items():
+                acc[k] = acc.get(k, 0) + int(v)
+        self.fb = fb
+        acc.update(trace_ms=0.0, trace_launches=0, process_ms=0.0, sort_ms=0.0, kernel_ms=0.0, passes=n)
+        return acc
+
+    def framebuffer(self):
+        return self.fb
+
+    def set_event_timing(self, on):
+        pass
+
+    def set_counters(self, on):
+        pass
+
+    def close(self):
+        pass
+
+
+class OracleInLibBackend(OracleBackend):
+    inlib = True
+
+    def __init__(self, log, n):
+        self.dist = self.torch = None
+        self.world, self.rank, self.local = n, 0, 0
+        self.device = None
+        self.use_dist = False
+        self.log = log
+
+    def renderer(self, scene, sort, tiles):
+        assert tiles is None
+        return OracleMulti(scene, sort, self.world)
+
+    def barrier_sync(self):
+        pass
+
+
+@pytest.mark.parametrize("n,steps", [(2, None), (3, 1)])
+def test_bench_run_in_library_backend(n, steps, monkeypatch):
+    """`--gpus N` without torchrun (WORLD_SIZE unset): bench.run over the in-library backend (one process,
+    rt_multi over N GPUs; here the oracle stands in) reports n_gpus == n_ranks_seen == N, and the timed
+    frame equals the single-process render bit for bit."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    sys.path.insert(0, REPO)
+    import bench
+    args = bench.parse_args(["--gpus", str(n), "--scene", "cornell_plus", "--warmup", "1", "--no-cpu-baseline"] +
+                            (["--steps", str(steps)] if steps else []))
+    log = []
+    buf = io.StringIO()
+    res = bench.run(args, OracleInLibBackend(log, n), cfg=CFG, json_out=buf)
+    line = json.loads(buf.getvalue().strip())
+    assert line["n_gpus"] == n and line["config"]["n_ranks_seen"] == n
+    assert "rt_multi" in line["config"]["launch"]
+    W, H, spp, bounces = CFG[1:5]
+    frame_spp = spp if steps is None else max(spp, 20 * n * steps)
+    assert line["steps"] == (-(-3 // n) if steps is None else steps)
+    if steps is None:
+        ref, _ = O.OracleScene(os.path.join(O.ASSETS, CFG[0]), image=(W, H, frame_spp, bounces)).render(
+            sort=True, threads=2)
+        assert np.array_equal(res["timed_fb"], ref)
+    assert res["my_passes"] == -(-frame_spp // 20)
+
+
+def test_bench_gpus_argument_is_checked():
+    """--gpus N is never ignored: WORLD_SIZE (torchrun) must equal it, and without torchrun N may not exceed
+    the visible HIP devices (none in this container): both exit with status 2 before any rendering."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--no-extras"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "HIP device(s) visible" in r.stderr, r.stderr[-2000:]
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3", "--no-extras"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr, r.stderr[-2000:]
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--no-extras"],
+                       env=dict(env, RTAMD_HW_QUEUES="40"), capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "1..32" in r.stderr

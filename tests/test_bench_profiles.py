@@ -54,25 +54,51 @@ def test_bench_line_fractions_at_most_one():
 
 
 def test_roofline_restated_on_exclusive_launches():
-    """bench.roofline (round 3): achieved = algorithmic bytes (scene once per XCD) / the exclusive launch
-    duration; traffic_frac = the PMC bytes over the same duration; the shared-chip spans only in `shared`."""
+    """bench.roofline: the exclusive-launch figures (round 3) are a labelled secondary field -- achieved =
+    algorithmic bytes (scene once per XCD) / the exclusive launch duration; traffic_frac = the PMC bytes over
+    the same duration; the shared-chip spans only in `shared`."""
     bench = _bench()
     counted = {"live_segments": 79_000_000, "generated_rays": 41_472_000, "nodes_popped": 800_000_000,
                "internal_visits": 680_000_000, "triangle_tests": 300_000_000}
     excl = {"launches": 16, "ms_per_launch": 0.7, "trace_ms": 11.2, "kernel_ms": 15.0, "counted": counted}
     scene_bytes = 32 * 252_099 + 48 * 126_050
     roof = bench.roofline(excl, counted, 16, 2.3, scene_bytes, 0, WORKLOAD, 0.14, 20)
+    ex = roof["exclusive"]
     comp = (24 * (79_000_000 - 41_472_000) + 8 * 79_000_000 + 16 * 8 * scene_bytes) / 16
-    assert roof["bytes_per_launch"] == int(comp)
-    assert abs(roof["achieved"] - comp / 0.7e-3 / 1e9) < 0.1
-    assert abs(roof["frac"] - roof["achieved"] / 8000.0) < 1e-4
-    assert roof["shared"]["ms_per_launch"] == 2.3 and roof["ms_per_launch"] == 0.7
+    assert ex["bytes_per_launch"] == int(comp)
+    assert abs(ex["achieved"] - comp / 0.7e-3 / 1e9) < 0.1
+    assert abs(ex["frac"] - ex["achieved"] / 8000.0) < 1e-4
+    assert roof["shared"]["ms_per_launch"] == 2.3 and ex["ms_per_launch"] == 0.7
     pmc = bench.load_pmc(WORKLOAD)
     if pmc:
-        assert abs(roof["traffic_frac"] - pmc["trace_bytes_per_launch"] / 0.7e-3 / 1e9 / 8000.0) < 1e-3
+        assert abs(ex["traffic_frac"] - pmc["trace_bytes_per_launch"] / 0.7e-3 / 1e9 / 8000.0) < 1e-3
     assert roof["logical_per_step"]["achieved"] > 0
 
 
+def test_roofline_headline_fits_the_step():
+    """Round 6 (verdict r05 item 3): the headline achieved / frac / traffic / traffic_frac are the timed-step
+    figures: frac x peak x the kernel's time per step = the step's algorithmic trace bytes, that time is at most
+    ms_per_step, and traffic_frac prices the measured bytes of one pass over the same time."""
+    bench = _bench()
+    counted = {"live_segments": 20 * 79_000_000, "generated_rays": 20 * 41_472_000, "nodes_popped": 1,
+               "internal_visits": 1, "triangle_tests": 1}
+    excl = {"launches": 16, "ms_per_launch": 0.7, "trace_ms": 11.2, "kernel_ms": 15.0, "counted": counted}
+    scene_bytes = 32 * 252_099 + 48 * 126_050
+    elapsed, steps = 0.118, 20
+    roof = bench.roofline(excl, counted, 20 * 16, 2.3, scene_bytes, 0, WORKLOAD, elapsed, steps)
+    t = roof["timed"]
+    assert roof["regime"] == "timed step" and roof["frac"] == t["frac"] and roof["achieved"] == t["achieved"]
+    step_ms = elapsed / steps * 1e3
+    assert 0 < roof["kernel_ms_per_step"] <= step_ms
+    alg_step = bench.compulsory_trace_bytes(counted, scene_bytes, 20 * 16, per_xcd=True) / steps
+    assert roof["bytes_per_step"] == int(alg_step)
+    assert abs(roof["frac"] * roof["peak"] * 1e9 * roof["kernel_ms_per_step"] / 1e3 - alg_step) / alg_step < 2e-3
+    # at most the step's algorithmic bytes at the HBM peak over the whole step
+    assert roof["frac"] * roof["peak"] * 1e9 * roof["kernel_ms_per_step"] / 1e3 <= alg_step * 1.002
+    pmc = bench.load_pmc(WORKLOAD)
+    assert roof["traffic"] == t["measured_bytes_per_step"]
+    assert abs(roof["traffic_frac"] - pmc["trace_bytes_per_launch"] * pmc["trace_launches"] /
+               (roof["kernel_ms_per_step"] / 1e3) / 1e9 / 8000.0) < 2e-3
 
 
 def _final_lines():
@@ -108,7 +134,8 @@ def test_closing_exclusive_launch_agrees_with_the_profiler():
     """The bench's exclusive trace launch duration (device wall clock, one atomic per workgroup) and the
     profiler's average dispatch duration of the same launches agree within 10 %."""
     roof = _final_lines()["bench_teapot.json"]["roofline"]
-    a, b = roof["ms_per_launch"], roof["pmc_run"]["ms_per_launch"]
+    ex = roof.get("exclusive", roof)          # round 6: the exclusive figures moved under `exclusive`
+    a, b = ex["ms_per_launch"], ex["pmc_run"]["ms_per_launch"]
     assert abs(a - b) / b < 0.10, (a, b)
 
 

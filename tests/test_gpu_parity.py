@@ -220,7 +220,7 @@ def test_multi_device_loopback_bitexact(gpu, monkeypatch, world, scene, image, s
     rt_multi.hip's device threads on the same GPU with its two collectives as device-to-device copies (RCCL refuses
     two ranks on one GPU), so the pass dealing, the stale rows of rounds a device has no pass in, the overlapped
     exchange, the owners' ordered adds and the gather all run at N = 2 / 3 / 5: bit-exact against the oracle."""
-    monkeypatch.setenv("RTAMD_MULTI_LOOPBACK", "1")
+    monkeypatch.setenv("RTAMD_MULTI_LOOPBACK", "1")   # read by the test build only (librtamd_test.so)
     if xchg != "overlap-1call":
         monkeypatch.setenv("RTAMD_XCHG_CHUNK", "16")
     if xchg == "sync":
@@ -229,11 +229,15 @@ def test_multi_device_loopback_bitexact(gpu, monkeypatch, world, scene, image, s
         monkeypatch.setenv("RTAMD_XCHG_ROUNDS", "1")
     osc, psc = _pair(scene, image)
     ofb, ost = osc.render(sort=sort)
-    gfb, gst = R.render(psc, sort=sort, devices=[0] * world)
+    T = R.test_lib()
+    gfb, gst = R.render(psc, sort=sort, devices=[0] * world, L=T)
     assert np.array_equal(gfb, ofb), _diff(gfb, ofb)
     assert gst["live_segments"] == ost["live_segments"] and gst["passes"] == psc.passes
     with pytest.raises(R.RtError, match="pass sharding only"):
-        R.render(psc, sort=sort, devices=[0] * world, shard_tiles=True)
+        R.render(psc, sort=sort, devices=[0] * world, shard_tiles=True, L=T)
+    # the product library has no loopback transport: the same device list is refused
+    with pytest.raises(R.RtError, match="twice"):
+        R.render(psc, sort=sort, devices=[0] * world)
 
 
 def test_multi_device_rejects_bad_device_lists(gpu):

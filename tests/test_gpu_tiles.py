@@ -175,14 +175,17 @@ def test_library_tile_shard_one_device(gpu, sort):
 
 @pytest.mark.parametrize("shard_tiles", [False, True])
 def test_multi_device_failure_after_setup_returns(gpu, monkeypatch, shard_tiles):
-    """A device failing after the setup barrier (RTAMD_FAIL_AFTER_SETUP) makes rt_render return its
-    error; the device aborts only its own communicator (no call can race the abort)."""
+    """A device failing after the setup barrier (RTAMD_FAIL_AFTER_SETUP, a hook of the test build
+    librtamd_test.so) makes rt_render return its error; the device aborts only its own communicator
+    (no call can race the abort).  The product library ignores the variable."""
     monkeypatch.setenv("RTAMD_FAIL_AFTER_SETUP", "0")
     psc = R.Scene("%s/cornell.scene" % R.ASSETS, image=(32, 32, 8, 2))
+    T = R.test_lib()
     with pytest.raises(R.RtError, match="injected failure"):
-        R.render(psc, sort=True, devices=[0], shard_tiles=shard_tiles)
+        R.render(psc, sort=True, devices=[0], shard_tiles=shard_tiles, L=T)
+    fb, _ = R.render(psc, sort=True, devices=[0], shard_tiles=shard_tiles)   # no hook in the product
     monkeypatch.delenv("RTAMD_FAIL_AFTER_SETUP")
-    fb, _ = R.render(psc, sort=True, devices=[0], shard_tiles=shard_tiles)   # the library still works
+    fb, _ = R.render(psc, sort=True, devices=[0], shard_tiles=shard_tiles, L=T)   # the library still works
     ref, _ = O.OracleScene("%s/cornell.scene" % R.ASSETS, image=(32, 32, 8, 2)).render(sort=True)
     assert np.array_equal(fb, ref)
 
