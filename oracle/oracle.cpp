@@ -551,7 +551,18 @@ struct Counters {
     uint64_t pn = 0, iv = 0, tt = 0, st = 0, ht = 0, hs = 0, miss = 0, live = 0, dead = 0;
     uint32_t max_stack = 0, max_ray_pn = 0;
     uint32_t max_ray_steps = 0;   // internal visits + triangle tests of one ray (the HIP trace's steps)
+    // analysis only (tools/chain_models.py): the longest ray's dependent record fetches under trace-kernel
+    // models -- [0] one fetch per internal step (root free) and per triangle (the round-5 kernel); [1] two-level
+    // records (a descent fetches its node's record and its children's pair together, so a fetch serves two
+    // levels; a stack pop fetches one level) with two triangles per fetch; [2] the same with the children's pair
+    // index kept on the stack (pops fetch two levels too); [3] as [1] with one triangle per fetch
+    uint32_t max_chain[4] = {0, 0, 0, 0};
+    uint64_t sum_chain[4] = {0, 0, 0, 0};
     void add(const Counters &o) {
+        for (int k = 0; k < 4; k++) {
+            max_chain[k] = std::max(max_chain[k], o.max_chain[k]);
+            sum_chain[k] += o.sum_chain[k];
+        }
         pn += o.pn; iv += o.iv; tt += o.tt; st += o.st; ht += o.ht; hs += o.hs; miss += o.miss;
         live += o.live; dead += o.dead; max_stack = std::max(max_stack, o.max_stack);
         max_ray_pn = std::max(max_ray_pn, o.max_ray_pn);
@@ -568,12 +579,33 @@ void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index,
     idx_stack[0] = 0;
     dist_stack[0] = 0;
     const int sphere_count = (int)s->spheres.size();
+    uint32_t ch[4] = {0, 0, 0, 0};   // chain models (Counters::max_chain), analysis only
+    bool desc = false, cover1 = false, cover2 = false, root = true;
     while (sc) {
         sc--;
         const float dist = dist_stack[sc];
+        const bool desc_now = desc;
+        desc = false;
         if (dist >= closest) continue;
         const BvhNode &node = s->bvh[idx_stack[sc]];
         c.pn++;
+        if (is_leaf(node)) {
+            const uint32_t nt = (uint32_t)std::max(0, node.child1 - node.child2);
+            ch[0] += nt; ch[1] += (nt + 1) / 2; ch[2] += (nt + 1) / 2; ch[3] += nt;
+            cover1 = cover2 = false;
+        } else if (root) {
+            cover1 = cover2 = false;       // the root's record is in scalar registers: no fetch
+        } else {
+            ch[0]++;
+            // [1]/[3]: covered when this is the descent of a node whose fetch brought its children's pair
+            const bool c1 = desc_now && cover1;
+            if (!c1) { ch[1]++; ch[3]++; }
+            cover1 = !c1 && desc_now;      // a descent's fetch (mode B) brings the pair; a pop's does not
+            const bool c2 = desc_now && cover2;
+            if (!c2) ch[2]++;
+            cover2 = !c2;                  // [2]: every fetch brings the pair
+        }
+        root = false;
         if (is_leaf(node)) {
             for (int i = node.child2; i < node.child1; i++) {
                 c.tt++;
@@ -601,8 +633,13 @@ void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index,
             } else if (h2) {
                 idx_stack[sc] = node.child2; dist_stack[sc] = d2; sc++;
             }
+            desc = h1 || h2;
             if ((uint32_t)sc > c.max_stack) c.max_stack = (uint32_t)sc;
         }
+    }
+    for (int k = 0; k < 4; k++) {
+        c.max_chain[k] = std::max(c.max_chain[k], ch[k]);
+        c.sum_chain[k] += ch[k];
     }
 }
 
@@ -765,7 +802,8 @@ int pass_total(const orc_scene *s) { return (s->ray_count + 19) / 20; }
 
 // One GPU-semantics pass: generate, bounces (process + stable sort), per-pixel ordered sum.
 void gpu_pass(const orc_scene *s, int p, bool sort, float *pass_sum, Counters &total, uint64_t *hist,
-              uint64_t *sorted, int threads, uint32_t *bounce_max_steps = nullptr, uint64_t *bounce_live = nullptr) {
+              uint64_t *sorted, int threads, uint32_t *bounce_max_steps = nullptr, uint64_t *bounce_live = nullptr,
+              uint64_t *bounce_chains = nullptr) {
     int rtc, rem;
     pass_params(s, p, &rtc, &rem);
     const int64_t n = (int64_t)rtc * s->width * s->height;
@@ -796,6 +834,11 @@ void gpu_pass(const orc_scene *s, int p, bool sort, float *pass_sum, Counters &t
             for (auto &c : per) bc.add(c);
             if (bounce_max_steps) bounce_max_steps[b] = bc.max_ray_steps;
             if (bounce_live) bounce_live[b] = bc.live;
+            if (bounce_chains)
+                for (int k = 0; k < 4; k++) {
+                    bounce_chains[(size_t)b * 8 + k] = bc.max_chain[k];
+                    bounce_chains[(size_t)b * 8 + 4 + k] = bc.sum_chain[k];
+                }
         }
         for (auto &c : per) total.add(c);
         if (hist) {
@@ -1056,6 +1099,19 @@ int orc_pass_bounce_profile(const orc_scene *s, int sort, int pass, uint32_t *ma
     Counters total;
     uint64_t sorted = 0;
     gpu_pass(s, pass, sort != 0, sum.data(), total, nullptr, &sorted, threads, max_steps, live);
+    return 0;
+}
+
+// Analysis only (tools/chain_models.py): per bounce of pass p, the longest ray's dependent record fetches and
+// their sum over the live rays under the trace-kernel models of Counters::max_chain: out[b*8 + k] = max,
+// out[b*8 + 4 + k] = sum, k < 4.
+int orc_pass_chain_profile(const orc_scene *s, int sort, int pass, uint64_t *out, int threads) {
+    if (pass < 0 || pass >= pass_total(s)) { g_err = "pass range"; return -1; }
+    const int64_t pixels = (int64_t)s->width * s->height;
+    std::vector<float> sum(pixels * 3);
+    Counters total;
+    uint64_t sorted = 0;
+    gpu_pass(s, pass, sort != 0, sum.data(), total, nullptr, &sorted, threads, nullptr, nullptr, out);
     return 0;
 }
 
