@@ -52,6 +52,28 @@ int main(int argc, char **argv) {
                     (unsigned long long)st.live_segments, q ? q : "unset");
         std::fflush(stdout);
     }
+    // the same passes on one persistent renderer, three runs back to back (what a host rendering several frames
+    // would do): the first run pays what a fresh renderer pays, the later ones show the steady state
+    {
+        rt_opts o;
+        rt_default_opts(&o);
+        rt_renderer *r = nullptr;
+        if (rt_renderer_create(s, &o, &r) || rt_renderer_set_event_timing(r, 0)) {
+            std::printf("Error rt_renderer_create %s\n", rt_last_error());
+            return 1;
+        }
+        for (int k = 0; k < 3; k++) {
+            rt_stats st;
+            if (rt_renderer_run(r, 0, passes, 1, nullptr, &st)) {
+                std::printf("Error rt_renderer_run %s\n", rt_last_error());
+                return 1;
+            }
+            std::printf("{\"persistent_run\": %d, \"passes\": %u, \"kernel_ms\": %.3f, \"ms_per_pass\": %.4f}\n", k,
+                        st.passes, st.kernel_ms, st.kernel_ms / st.passes);
+            std::fflush(stdout);
+        }
+        rt_renderer_destroy(r);
+    }
     rt_opts o;
     rt_default_opts(&o);
     o.pass_count = 1;

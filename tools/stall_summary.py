@@ -20,7 +20,7 @@ for flag in ("--json", "--workload", "--run"):
 disp = collect(argv)
 per = collections.OrderedDict()
 for (k, i), d in disp.items():
-    if k.startswith("trace_kernel") or k.startswith("shade_kernel"):
+    if k.startswith(("trace_kernel", "trace2_kernel", "shade_kernel")):
         per.setdefault(k, []).append(d)
 print("# Wave time breakdown (tools/pmc.sh %s tools/pmc_groups/stall.txt; one teapot pass at 1080p, kernels\n"
       "# serialised by the profiler).  Fractions are of SQ_WAVE_CYCLES (the waves' resident time); instruction\n"
@@ -48,7 +48,7 @@ if "--json" in opts:
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS",
                   "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"):
             tot[c] += d.get(c, 0)
-            if k.startswith("trace_kernel"):
+            if k.startswith(("trace_kernel", "trace2_kernel")):
                 trace[c] += d.get(c, 0)
     path = opts["--json"] if os.path.isabs(opts["--json"]) else os.path.join(REPO, opts["--json"])
     try:
