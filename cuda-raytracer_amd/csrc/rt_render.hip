@@ -113,6 +113,7 @@ constexpr int kInflight = RT_INFLIGHT; // passes in flight (one stream and buffe
 constexpr int kStaggerUs = 4000;       // staggered start of the first passes in flight (rt_renderer::run):
 constexpr int kStaggerGroup = 4;       // the first kStaggerGroup together, then one every kStaggerUs
 constexpr int kStaggerMinPasses = 8;   // ...for renders of at least this many passes
+constexpr int kStaggerShortUs = 2000;  // the same for runs shorter than the passes in flight (run_impl)
 // Persistent trace grid as a % of the resident trace workgroups: the passes in flight share the
 // chip, so each pass's trace takes 200 % / (passes in flight), at least RT_TRACE_OCC_MIN and at most
 // 100 % (20 in flight: 15 %; A/B at 20 in flight: 40 % 7.51, 30 % 7.41, 20 % 7.37, 15 % 7.33,
@@ -1538,6 +1539,8 @@ struct rt_renderer {
     bool shade_hist = !std::getenv("RTAMD_SHADE_HIST") || std::atoi(std::getenv("RTAMD_SHADE_HIST")) != 0;
     int stagger_us = std::getenv("RTAMD_STAGGER_US") ? std::max(0, std::min(20000, std::atoi(std::getenv("RTAMD_STAGGER_US"))))
                                                     : kStaggerUs;
+    int short_stagger_us = std::getenv("RTAMD_STAGGER_SHORT_US")
+                               ? std::max(0, std::min(20000, std::atoi(std::getenv("RTAMD_STAGGER_SHORT_US")))) : kStaggerShortUs;
     PassCtx ctx[kInflight];
     int pass_hint = 0;                // rt_render: the passes this renderer will ever run (0: any)
     int inflight_limit = 0;           // a cap on passes in flight set by the creator (rt_multi next to RCCL)
@@ -2351,11 +2354,19 @@ struct rt_renderer {
             // staggered, one pass's tail overlaps another's heavy bounces (A/B: 20-pass batch 7.13 ->
             // 7.02 ms/pass, through the dist path 7.40 -> 7.19, full frame 6.84 -> 6.74, lamp 20 steps
             // 13.53 -> 13.32; one pass every 2 ms from pass 1: 7.23 -> 7.14).  Later passes start when a
-            // context frees, staggered already.  Only for renders of at least as many passes as may be
-            // in flight (kInflight, or RTAMD_INFLIGHT): a shorter one (cornell_plus' 13 passes of 3 ms)
-            // only waits (3.04 -> 3.49 ms/pass), as does a 13-pass rank share at 16 in flight (7.52 -> 7.61).  RTAMD_STAGGER_US / RTAMD_STAGGER_GROUP
-            // override.
-            const long stagger_ticks = count >= inflight_cap && count >= kStaggerMinPasses ? (long)stagger_us * wall_khz / 1000 : 0;
+            // context frees, staggered already.  RTAMD_STAGGER_US / RTAMD_STAGGER_GROUP override.  At 4 ms,
+            // runs shorter than the passes in flight only waited (round 4: cornell_plus' 13 passes of 3 ms
+            // 3.04 -> 3.49 ms/pass, a 13-pass rank share at 16 in flight 7.52 -> 7.61).
+            // Round 6: such a run (a rank's 13-pass share of a frame at N = 8) is one batch with no steady
+            // state; its passes start kStaggerShortUs apart, scaled by the rays per pass (a 1080p pass = 1;
+            // cornell_plus' 512^2 passes start ~0.25 ms apart).  A/B, teapot 13-pass share:
+            // 6.42 -> 6.25 ms/pass (20 in flight), 6.53 -> 6.36 through torch.distributed at 16 in flight;
+            // 2 ms for the long runs as well was worse (26 passes: 6.07 -> 6.16).  RTAMD_STAGGER_SHORT_US overrides.
+            const int64_t rays_per_pass = (int64_t)std::min(spp - 20 * pass_begin, 20) * tile_pixels();
+            const double short_us = short_stagger_us * std::min(1.0, (double)rays_per_pass / (1920.0 * 1080.0 * 20.0));
+            const long stagger_ticks = count < kStaggerMinPasses ? 0
+                                       : count >= inflight_cap ? (long)stagger_us * wall_khz / 1000
+                                                               : (long)(short_us * wall_khz / 1000);
             const int stagger_group = std::getenv("RTAMD_STAGGER_GROUP") ? std::max(1, std::atoi(std::getenv("RTAMD_STAGGER_GROUP")))
                                                                         : kStaggerGroup;
             for (int k = 0; k < count; k++) {
