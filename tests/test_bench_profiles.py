@@ -1,6 +1,6 @@
 """The committed PMC summaries that bench.py prices its roofline with (profiles/pmc_traffic.json,
 profiles/pmc_issue.json) are present for the headline workload, come from exactly one profiled pass,
-and give fractions <= 1 at the measured pass time (the closing bench lines measured with them: profiles/r05/final)."""
+and give fractions <= 1 at the measured pass time (the closing bench lines measured with them: profiles/r06/final)."""
 import importlib
 import json
 import os
@@ -8,7 +8,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKLOAD = "teapot.scene 1920x1080 2048spp 16 bounces sort=on"
-FINAL = os.path.join(REPO, "profiles", "r05", "final")   # the closing measurement of this round
+FINAL = os.path.join(REPO, "profiles", "r06", "final")   # the closing measurement of this round
 
 
 def _bench():
@@ -51,6 +51,22 @@ def test_bench_line_fractions_at_most_one():
     t = roof["timed"]                                   # round 5: the trace kernel inside the timed step
     assert 0 < t["ms_per_step"] <= t["step_ms"] and 0 < t["frac"] <= 1 and 0 < t["measured_frac"] <= 1
     assert 0 < t["valu_frac"] <= 1
+
+
+def test_closing_headline_is_the_timed_step():
+    """Round 6 (verdict r05 item 3): the closing lines' headline achieved / frac are the timed-step figures: frac x peak
+    x the kernel's time per step recomputes the step's algorithmic trace bytes, and that time fits in ms_per_step.  The
+    exclusive-launch figures sit under `exclusive`, and the PMC record is the measured revision's."""
+    rev = open(os.path.join(FINAL, "REVISION")).read().strip()
+    for name in ("bench_teapot.json", "bench_teapot_steps20.json"):
+        line = _final_lines()[name]
+        roof = line["roofline"]
+        assert roof["regime"] == "timed step" and roof["frac"] == roof["timed"]["frac"]
+        assert 0 < roof["kernel_ms_per_step"] <= line["ms_per_step"]
+        rebuilt = roof["frac"] * roof["peak"] * 1e9 * roof["kernel_ms_per_step"] / 1e3
+        assert abs(rebuilt - roof["bytes_per_step"]) / roof["bytes_per_step"] < 3e-3, name
+        assert roof["exclusive"]["ms_per_launch"] * roof["exclusive"]["launches"] > line["ms_per_step"]   # another regime
+    assert _bench().load_pmc(WORKLOAD)["run"].startswith("rev " + rev)
 
 
 def test_roofline_restated_on_exclusive_launches():

@@ -13,7 +13,7 @@ the passes): the Monte-Carlo noise floor.  Any implementation that differs from 
 by fast-math rounding differs from it by about the first figure; no implementation can reach a
 per-pixel tolerance below it.
 
-    python tools/fastmath_floor.py [--out profiles/r05/fastmath_floor.json]
+    python tools/fastmath_floor.py [--out docs/history/profiles/r04/fastmath_floor.json]
 """
 import argparse
 import json

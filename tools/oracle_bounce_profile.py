@@ -3,7 +3,7 @@ infrastructure): the longest ray's trace steps (internal visits + triangle tests
 step each) and the live rays per bounce -- the floor of a latency-bound tail bounce is that
 longest ray's chain of dependent steps.
 
-    python tools/oracle_bounce_profile.py teapot [pass ...] > profiles/r05/oracle_bounce_profile_teapot.json"""
+    python tools/oracle_bounce_profile.py teapot [pass ...] > /tmp/oracle_bounce_profile_teapot.json"""
 import json
 import os
 import sys

@@ -2,7 +2,7 @@
 BASELINE config x GPUs.  1-GPU cells come from profiles/<round>/bench_*.json and profiles/pmc_traffic.json;
 N > 1 has no hardware measurement (the driver's SCALE run is the only one), so those rows say so.
 
-    python tools/results_table.py [profiles/r05/final]"""
+    python tools/results_table.py [profiles/r06/final]"""
 import json
 import os
 import sys
