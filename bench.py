@@ -56,7 +56,8 @@ def _argv_gpus(argv):
     return 1
 
 
-_DIST = int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dist" in sys.argv or _argv_gpus(sys.argv) > 1
+_DIST = (int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dist" in sys.argv or "--inlib" in sys.argv or
+         _argv_gpus(sys.argv) > 1)
 _HWQ = os.environ.get("RTAMD_HW_QUEUES")            # RTAMD_HW_QUEUES: sweeps only
 if _HWQ is not None and not (_HWQ.isdigit() and 1 <= int(_HWQ) <= 32):
     sys.exit("bench.py: RTAMD_HW_QUEUES=%r: expected a queue count in 1..32" % _HWQ)
@@ -563,6 +564,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-extras", action="store_true",
                     help="only the warmup and timed steps (profiling: --steps 1 --warmup 0 renders exactly one pass)")
     ap.add_argument("--dist", action="store_true", help="use the torch.distributed path even at N=1")
+    ap.add_argument("--inlib", action="store_true",
+                    help="use the library's in-process multi-GPU renderer (rt_multi) even at N=1 (without torchrun)")
     ap.add_argument("--shard", choices=("passes", "tiles"), default="passes",
                     help="multi-GPU decomposition: whole passes per GPU or 8-row pixel stripes per GPU over "
                          "every pass (sort on: one byte per live ray all-reduced after every bounce); both exact")
@@ -883,7 +886,9 @@ def make_backend(args):
     n = args.gpus if args.gpus is not None else 1
     if n < 1:
         raise SystemExit2("bench.py: --gpus must be at least 1")
-    if n > 1:
+    if args.dist and args.inlib:
+        raise SystemExit2("bench.py: --dist and --inlib are exclusive")
+    if n > 1 or args.inlib:
         if args.dist:
             raise SystemExit2("bench.py: --dist with --gpus > 1 needs torchrun (one process per GPU)")
         return InLibBackend(n)
