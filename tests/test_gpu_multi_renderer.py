@@ -88,3 +88,15 @@ def test_bench_gpus2_without_torchrun_loopback(tmp_path):
     assert "rt_multi" in line["config"]["launch"] and "loopback" in line["config"]["launch"]
     assert line["parity"]["frame_bit_exact_vs_oracle"] is True
     assert line["bit_exact_vs_oracle"] is True
+
+
+def test_bench_inlib_one_gpu_rccl():
+    """`bench.py --inlib` at N = 1: the product library's rt_multi over a one-device RCCL communicator (the path
+    `--gpus N` takes without torchrun); the timed cornell_plus frame equals the oracle's frame hash."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "RTAMD_LIB")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--inlib", "--scene", "cornell_plus",
+                        "--warmup", "1", "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["config"]["n_ranks_seen"] == 1 and "rt_multi" in line["config"]["launch"]
+    assert line["parity"]["frame_bit_exact_vs_oracle"] is True and line["bit_exact_vs_oracle"] is True
