@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <sstream>
 #include <string>
 #include <unordered_map>
@@ -558,7 +559,10 @@ struct Counters {
     // index kept on the stack (pops fetch two levels too); [3] as [1] with one triangle per fetch
     uint32_t max_chain[4] = {0, 0, 0, 0};
     uint64_t sum_chain[4] = {0, 0, 0, 0};
+    // analysis only: pushes the HIP trace kernel makes below its 8 LDS entries (global overflow stack)
+    uint64_t ovf = 0;
     void add(const Counters &o) {
+        ovf += o.ovf;
         for (int k = 0; k < 4; k++) {
             max_chain[k] = std::max(max_chain[k], o.max_chain[k]);
             sum_chain[k] += o.sum_chain[k];
@@ -570,6 +574,18 @@ struct Counters {
     }
 };
 
+// Analysis instrumentation of the traversal (chain models, fetch records, overflow pushes): compiled into the
+// strict liboracle.so only (-DORC_ANALYSIS), never into the timed cpu_baseline or the fast-math studies.
+#ifdef ORC_ANALYSIS
+#define ORC_A(...) __VA_ARGS__
+#else
+#define ORC_A(...)
+#endif
+// analysis only (orc_bounce_working_set): the records one traversal fetches, in order -- an internal node's id
+// (its child-pair record), or kRecTri | triangle index; the root's record is free (scalar registers)
+constexpr uint32_t kRecTri = 0x80000000u;
+thread_local std::vector<uint32_t> *g_rec = nullptr;
+
 // ---------------------------------------------------------------- scene.cu:134-241
 void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index, Counters &c) {
     const V3 n_inv{FDIV(1.0f, d.x), FDIV(1.0f, d.y), FDIV(1.0f, d.z)};
@@ -579,16 +595,16 @@ void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index,
     idx_stack[0] = 0;
     dist_stack[0] = 0;
     const int sphere_count = (int)s->spheres.size();
-    uint32_t ch[4] = {0, 0, 0, 0};   // chain models (Counters::max_chain), analysis only
-    bool desc = false, cover1 = false, cover2 = false, root = true;
+    ORC_A(uint32_t ch[4] = {0, 0, 0, 0};   // chain models (Counters::max_chain), analysis only
+          bool desc = false, cover1 = false, cover2 = false, root = true;)
     while (sc) {
         sc--;
         const float dist = dist_stack[sc];
-        const bool desc_now = desc;
-        desc = false;
+        ORC_A(const bool desc_now = desc; desc = false;)
         if (dist >= closest) continue;
         const BvhNode &node = s->bvh[idx_stack[sc]];
         c.pn++;
+#ifdef ORC_ANALYSIS
         if (is_leaf(node)) {
             const uint32_t nt = (uint32_t)std::max(0, node.child1 - node.child2);
             ch[0] += nt; ch[1] += (nt + 1) / 2; ch[2] += (nt + 1) / 2; ch[3] += nt;
@@ -596,6 +612,7 @@ void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index,
         } else if (root) {
             cover1 = cover2 = false;       // the root's record is in scalar registers: no fetch
         } else {
+            if (g_rec) g_rec->push_back(idx_stack[sc]);
             ch[0]++;
             // [1]/[3]: covered when this is the descent of a node whose fetch brought its children's pair
             const bool c1 = desc_now && cover1;
@@ -606,9 +623,11 @@ void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index,
             cover2 = !c2;                  // [2]: every fetch brings the pair
         }
         root = false;
+#endif
         if (is_leaf(node)) {
             for (int i = node.child2; i < node.child1; i++) {
                 c.tt++;
+                ORC_A(if (g_rec) g_rec->push_back(kRecTri | (uint32_t)i);)
                 float t;
                 if (ray_tri(s->triangles[i], o, d, closest, &t)) {
                     closest = t;
@@ -621,6 +640,7 @@ void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index,
             const bool h1 = ray_aabb(s->bvh[node.child1].aabb, o, n_inv, d1, closest);
             const bool h2 = ray_aabb(s->bvh[node.child2].aabb, o, n_inv, d2, closest);
             if (h1 && h2) {
+                ORC_A(if (sc >= 8) c.ovf++;)   // the kernel pushes one child here, at entry sc
                 if (d1 < d2) {
                     idx_stack[sc] = node.child1; dist_stack[sc] = d1; sc++;
                     idx_stack[sc] = node.child2; dist_stack[sc] = d2; sc++;
@@ -633,14 +653,16 @@ void bvh_closest_hit(const orc_scene *s, V3 o, V3 d, float &closest, int &index,
             } else if (h2) {
                 idx_stack[sc] = node.child2; dist_stack[sc] = d2; sc++;
             }
-            desc = h1 || h2;
+            ORC_A(desc = h1 || h2;)
             if ((uint32_t)sc > c.max_stack) c.max_stack = (uint32_t)sc;
         }
     }
+#ifdef ORC_ANALYSIS
     for (int k = 0; k < 4; k++) {
         c.max_chain[k] = std::max(c.max_chain[k], ch[k]);
         c.sum_chain[k] += ch[k];
     }
+#endif
 }
 
 // ---------------------------------------------------------------- scene.cu:284-318
@@ -801,6 +823,10 @@ void pass_params(const orc_scene *s, int p, int *rtc, int *remaining_after) {
 int pass_total(const orc_scene *s) { return (s->ray_count + 19) / 20; }
 
 // One GPU-semantics pass: generate, bounces (process + stable sort), per-pixel ordered sum.
+// analysis only: called before bounce b with the pass's rays, slot -> ray and slot keys; true stops the pass
+std::function<bool(int, const std::vector<RayData> &, const std::vector<uint32_t> &, const std::vector<uint32_t> &)>
+    g_bounce_hook;
+
 void gpu_pass(const orc_scene *s, int p, bool sort, float *pass_sum, Counters &total, uint64_t *hist,
               uint64_t *sorted, int threads, uint32_t *bounce_max_steps = nullptr, uint64_t *bounce_live = nullptr,
               uint64_t *bounce_chains = nullptr) {
@@ -813,6 +839,7 @@ void gpu_pass(const orc_scene *s, int p, bool sort, float *pass_sum, Counters &t
 #pragma omp parallel for schedule(static) num_threads(nt)
     for (int64_t i = 0; i < n; i++) generate_ray(s, rays.data(), idx.data(), keys.data(), rtc, (int)i, rem);
     for (int b = 0; b < s->bounces; b++) {
+        if (g_bounce_hook && g_bounce_hook(b, rays, idx, keys)) return;
         const uint32_t seed = (uint32_t)(rem * 20 + b);
         std::vector<Counters> per(nt);
 #pragma omp parallel num_threads(nt)
@@ -1106,12 +1133,201 @@ int orc_pass_bounce_profile(const orc_scene *s, int sort, int pass, uint32_t *ma
 // their sum over the live rays under the trace-kernel models of Counters::max_chain: out[b*8 + k] = max,
 // out[b*8 + 4 + k] = sum, k < 4.
 int orc_pass_chain_profile(const orc_scene *s, int sort, int pass, uint64_t *out, int threads) {
+#ifndef ORC_ANALYSIS
+    g_err = "analysis build only (liboracle.so)";
+    return -1;
+#endif
     if (pass < 0 || pass >= pass_total(s)) { g_err = "pass range"; return -1; }
     const int64_t pixels = (int64_t)s->width * s->height;
     std::vector<float> sum(pixels * 3);
     Counters total;
     uint64_t sorted = 0;
     gpu_pass(s, pass, sort != 0, sum.data(), total, nullptr, &sorted, threads, nullptr, nullptr, out);
+    return 0;
+}
+
+// Analysis only (tools/route_model.py, verdict r05 item 6): which scene bytes the trace kernel's rays in flight on
+// one XCD touch at bounce `bounce` of pass p, under three ways of dealing the live slots to the 8 XCDs:
+//   policy 0  contiguous eighths of the slots (the product: queue shard = blockIdx % 8, blocks dealt round-robin
+//             over the XCDs, so an XCD's waves take the shard's slot range; after the reorder that range is a run of
+//             buckets, i.e. of origin octants of the scene box)
+//   policy 1  the x-th eighth of every bucket (round 5's XCD-affine order: a band of image rows)
+//   policy 2  by the first depth-`depth` subtree the ray's traversal enters (the top-level treelet), 2^depth
+//             treelets dealt to 8 XCDs round-robin
+// For each XCD, its rays are taken in slot order in windows of `window` rays (the lanes one XCD holds resident);
+// out (per policy, 6 doubles): mean and max over the sampled windows of the distinct bytes touched (64-B node
+// records + 48-B triangles), the mean fetched bytes per window, the largest XCD's share of the rays, and, over
+// the whole bounce, the scene bytes the 8 L2s miss (each 4 MB, 16-way LRU, 128-B lines, node records at 64 B
+// per node id and then the triangles at 48 B; every XCD's rays in slot order, one after another) and the
+// fetched bytes; then out[18..20] = the kernel's overflow-stack pushes over the bounce, the live rays, and the rays
+// with at least one.
+int orc_bounce_working_set(const orc_scene *s, int sort, int pass, int bounce, int window, int depth,
+                           int windows_per_xcd, double *out, int threads) {
+#ifndef ORC_ANALYSIS
+    g_err = "analysis build only (liboracle.so)";
+    return -1;
+#endif
+    if (pass < 0 || pass >= pass_total(s)) { g_err = "pass range"; return -1; }
+    if (bounce < 0 || bounce >= s->bounces || window < 1 || depth < 1 || depth > 12 || windows_per_xcd < 1) {
+        g_err = "bad arguments"; return -1;
+    }
+    const int nn = (int)s->bvh.size();
+    std::vector<int> dep(nn, 0), par(nn, -1);           // node depths and parents (children follow their parent)
+    for (int i = 0; i < nn; i++)
+        if (!is_leaf(s->bvh[i])) {
+            dep[s->bvh[i].child1] = dep[i] + 1;
+            dep[s->bvh[i].child2] = dep[i] + 1;
+            par[s->bvh[i].child1] = par[s->bvh[i].child2] = i;
+        }
+    const int nt = nthreads(threads);
+    bool done = false;
+    g_bounce_hook = [&](int b, const std::vector<RayData> &rays, const std::vector<uint32_t> &idx,
+                        const std::vector<uint32_t> &keys) {
+        if (b != bounce) return false;
+        done = true;
+        int64_t L = 0;                                  // live slots are a prefix after the reorder
+        while (L < (int64_t)keys.size() && keys[L] != 0xFFFFFFFFu) L++;
+        // per live slot: the records its traversal fetches (kept only for the slots a sampled window holds)
+        std::vector<int> xcd[3];
+        for (auto &v : xcd) v.assign(L, 0);
+        std::vector<int64_t> bstart(66, L);             // bucket ranges (policy 1)
+        for (int64_t k = L - 1; k >= 0; k--) bstart[orc_key_bucket(keys[k])] = k;
+        for (int bk = 64; bk >= 0; bk--) bstart[bk] = std::min(bstart[bk], bstart[bk + 1]);
+        std::vector<std::vector<uint32_t>> rec(L);
+        std::vector<int> first_sub(L, 0);
+        std::vector<uint64_t> ovf(L, 0);
+#pragma omp parallel for schedule(dynamic, 1024) num_threads(nt)
+        for (int64_t k = 0; k < L; k++) {
+            std::vector<uint32_t> r;
+            g_rec = &r;
+            float closest = 1e30f;
+            int index = -1;
+            Counters c;
+            const RayData &rd = rays[idx[k]];
+            bvh_closest_hit(s, rd.origin, rd.dir, closest, index, c);
+            g_rec = nullptr;
+            ovf[k] = c.ovf;
+            int sub = 0;
+            for (uint32_t x : r)
+                if (!(x & kRecTri) && dep[x] >= depth) {   // the first fetched node at the treelet depth or below
+                    int a = (int)x;
+                    while (dep[a] > depth) a = par[a];   // its depth-`depth` ancestor
+                    sub = a;
+                    break;
+                }
+            first_sub[k] = sub;
+            rec[k].swap(r);
+        }
+        std::unordered_map<int, int> sub_id;           // depth-`depth` subtrees in node order -> 0, 1, ...
+        {
+            std::vector<int> subs;
+            for (int i = 0; i < nn; i++) if (dep[i] == depth) subs.push_back(i);
+            for (size_t i = 0; i < subs.size(); i++) sub_id[subs[i]] = (int)i;
+        }
+        for (int64_t k = 0; k < L; k++) {
+            xcd[0][k] = (int)(k * 8 / L);
+            const int bk = orc_key_bucket(keys[k]);
+            const int64_t lo = bstart[bk], hi = bstart[bk + 1];
+            xcd[1][k] = (int)((k - lo) * 8 / std::max<int64_t>(1, hi - lo));
+            auto it = sub_id.find(first_sub[k]);
+            xcd[2][k] = it == sub_id.end() ? 0 : it->second % 8;
+        }
+        for (int pol = 0; pol < 3; pol++) {
+            std::vector<std::vector<int64_t>> seq(8);
+            for (int64_t k = 0; k < L; k++) seq[xcd[pol][k]].push_back(k);
+            size_t biggest = 0;
+            for (auto &q : seq) biggest = std::max(biggest, q.size());
+            std::vector<std::pair<int, int64_t>> wins;  // (xcd, first index in its sequence)
+            for (int x = 0; x < 8; x++) {
+                const int64_t m = (int64_t)seq[x].size();
+                if (m == 0) continue;
+                const int64_t nw = std::max<int64_t>(1, (m + window - 1) / window);
+                for (int w = 0; w < windows_per_xcd && w < nw; w++)
+                    wins.push_back({x, (nw * w / windows_per_xcd) * window});
+            }
+            std::vector<double> distinct(wins.size()), fetched(wins.size());
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+            for (int64_t wi = 0; wi < (int64_t)wins.size(); wi++) {
+                std::vector<uint8_t> seen_n(nn, 0), seen_t(s->triangles.size(), 0);
+                const auto &q = seq[wins[wi].first];
+                const int64_t a = wins[wi].second, e = std::min<int64_t>((int64_t)q.size(), a + window);
+                double db = 0, fb = 0;
+                for (int64_t j = a; j < e; j++)
+                    for (uint32_t x : rec[q[j]]) {
+                        const bool tri = x & kRecTri;
+                        const uint32_t i = x & ~kRecTri;
+                        fb += tri ? 48 : 64;
+                        uint8_t &sn = tri ? seen_t[i] : seen_n[i];
+                        if (!sn) { sn = 1; db += tri ? 48 : 64; }
+                    }
+                distinct[wi] = db;
+                fetched[wi] = fb;
+            }
+            double mean = 0, mx = 0, fm = 0;
+            for (size_t i = 0; i < wins.size(); i++) { mean += distinct[i]; mx = std::max(mx, distinct[i]); fm += fetched[i]; }
+            out[pol * 6 + 0] = wins.empty() ? 0 : mean / wins.size();
+            out[pol * 6 + 1] = mx;
+            out[pol * 6 + 2] = wins.empty() ? 0 : fm / wins.size();
+            out[pol * 6 + 3] = L ? (double)biggest / (double)L : 0;
+            // whole-bounce L2 model, one XCD per thread
+            constexpr int kWays = 16, kSets = (4 << 20) / 128 / kWays;
+            const uint64_t tri_base = (uint64_t)nn * 64;
+            std::vector<double> miss(8, 0), all(8, 0);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(std::min(nt, 8))
+            for (int x = 0; x < 8; x++) {
+                std::vector<uint64_t> tag((size_t)kSets * kWays, ~0ull), age((size_t)kSets * kWays, 0);
+                uint64_t clock = 0;
+                double ms = 0, fs = 0;
+                auto touch = [&](uint64_t line) {
+                    const size_t set = (size_t)(line % kSets) * kWays;
+                    clock++;
+                    size_t victim = set;
+                    for (size_t w = set; w < set + kWays; w++) {
+                        if (tag[w] == line) { age[w] = clock; return; }
+                        if (age[w] < age[victim]) victim = w;
+                    }
+                    tag[victim] = line;
+                    age[victim] = clock;
+                    ms += 128;
+                };
+                for (int64_t k : seq[x])
+                    for (uint32_t r : rec[k]) {
+                        const bool tri = r & kRecTri;
+                        const uint64_t a = tri ? tri_base + (uint64_t)(r & ~kRecTri) * 48 : (uint64_t)r * 64;
+                        const uint64_t b = a + (tri ? 47 : 63);
+                        fs += tri ? 48 : 64;
+                        touch(a / 128);
+                        if (b / 128 != a / 128) touch(b / 128);
+                    }
+                miss[x] = ms;
+                all[x] = fs;
+            }
+            double mt = 0, ft = 0;
+            for (int x = 0; x < 8; x++) { mt += miss[x]; ft += all[x]; }
+            out[pol * 6 + 4] = mt;
+            out[pol * 6 + 5] = ft;
+        }
+        {                                               // out[18..20]: overflow pushes, live rays, rays that overflow
+            uint64_t t = 0, r = 0;
+            for (int64_t k = 0; k < L; k++) { t += ovf[k]; r += ovf[k] != 0; }
+            out[18] = (double)t;
+            out[19] = (double)L;
+            out[20] = (double)r;
+        }
+        return true;
+    };
+    const int64_t pixels = (int64_t)s->width * s->height;
+    std::vector<float> sum(pixels * 3);
+    Counters total;
+    uint64_t sorted = 0;
+    try {
+        gpu_pass(s, pass, sort != 0, sum.data(), total, nullptr, &sorted, threads);
+    } catch (...) {
+        g_bounce_hook = nullptr;
+        throw;
+    }
+    g_bounce_hook = nullptr;
+    if (!done) { g_err = "bounce not reached"; return -1; }
     return 0;
 }
 

@@ -89,6 +89,12 @@ int orc_render_pass_sums(const orc_scene *s, int sort, int pass_begin, int pass_
  * (the HIP trace kernel's steps), live[b] = live rays.  Arrays of `bounces` entries. */
 int orc_pass_bounce_profile(const orc_scene *s, int sort, int pass, uint32_t *max_steps, uint64_t *live,
                             int threads);
+/* Analysis only: the longest ray's dependent record fetches per bounce under the chain models
+ * (tools/chain_models.py), and the distinct scene bytes one XCD's rays in flight touch under three ways of
+ * dealing the live slots to the XCDs (tools/route_model.py); see oracle.cpp. */
+int orc_pass_chain_profile(const orc_scene *s, int sort, int pass, uint64_t *out, int threads);
+int orc_bounce_working_set(const orc_scene *s, int sort, int pass, int bounce, int window, int depth,
+                           int windows_per_xcd, double *out, int threads);
 
 /* CPU-path semantics (raytracing.cu:122-163): bounce-invariant seed quirk, no keys,
  * no sort, sequential accumulate.  fb_out: W*H*3 (overwritten). pass_limit < 0 = all. */
