@@ -79,6 +79,20 @@ import numpy as np  # noqa: E402
 
 import rtamd  # noqa: E402
 
+def hip_runtimes():
+    """The HIP runtime and RCCL files mapped into this process (diagnostic: the torch.distributed path runs the
+    renderer on torch's bundled runtime, which torch loads first; librtamd loaded first does not make torch use
+    /opt/rocm's -- torch's copy has another soname, and the renderer then finds no device)."""
+    seen = set()
+    try:
+        for line in open("/proc/self/maps"):
+            f = line.split()[-1]
+            if "libamdhip64" in f or "librccl" in f:
+                seen.add(f)
+    except OSError:
+        pass
+    return sorted(seen)
+
 CONFIGS = {
     # name: (scene file, W, H, spp, bounces, sort, use_bvh)
     "teapot": ("teapot.scene", 1920, 1080, 2048, 16, True, True),
@@ -814,6 +828,7 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
                                                                    "frame" if frame_spp != spp else "")),
                 "passes_per_frame": P,
                 "n_ranks_seen": n_ranks_seen,
+                "hip_runtime": hip_runtimes(),
                 **({"frame_extended": "%d spp (%d passes) instead of %d, so that each of the %d GPUs renders its %d "
                                       "passes in one batch" % (frame_spp, P, spp, world, steps)}
                    if frame_spp != spp else {}),
