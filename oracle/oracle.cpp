@@ -1331,6 +1331,141 @@ int orc_bounce_working_set(const orc_scene *s, int sort, int pass, int bounce, i
     return 0;
 }
 
+// Analysis only (tools/wave_model.py): would a finer trace ORDER (not slot order: slots, seeds and results stay) make
+// the trace kernel's waves more coherent at bounce `bounce`?  Every live ray's fetch sequence (internal-node steps and
+// triangle steps) is replayed through one model wave of 64 lanes that refills idle lanes in order once `refill` are
+// idle (the kernel's rule), in two orders: (0) slot order; (1) within each run of `tile` slots, stably sorted by a
+// finer key (origin on a 2^obits grid per axis, direction on a 2^dbits grid, Morton-interleaved).  Per order, out[6]:
+// iterations, node-body iterations, triangle-body iterations, lane-steps (= the useful work, the same for both),
+// distinct 128-B record lines requested summed over iterations, and the steps of the longest ray.
+int orc_bounce_wave_model(const orc_scene *s, int sort, int pass, int bounce, int tile, int obits, int dbits,
+                          int refill, double *out, int threads) {
+#ifndef ORC_ANALYSIS
+    g_err = "analysis build only (liboracle.so)";
+    return -1;
+#endif
+    if (pass < 0 || pass >= pass_total(s)) { g_err = "pass range"; return -1; }
+    if (bounce < 0 || bounce >= s->bounces || tile < 1 || obits < 0 || obits > 5 || dbits < 0 || dbits > 5 ||
+        refill < 1 || refill > 64) {
+        g_err = "bad arguments"; return -1;
+    }
+    const int nt = nthreads(threads);
+    const int nn = (int)s->bvh.size();
+    bool done = false;
+    g_bounce_hook = [&](int b, const std::vector<RayData> &rays, const std::vector<uint32_t> &idx,
+                        const std::vector<uint32_t> &keys) {
+        if (b != bounce) return false;
+        done = true;
+        int64_t L = 0;
+        while (L < (int64_t)keys.size() && keys[L] != 0xFFFFFFFFu) L++;
+        std::vector<std::vector<uint32_t>> rec(L);
+        std::vector<uint32_t> fine(L);
+        auto q = [](float v, int bits) {
+            const float x = std::min(std::max(v, 0.0f), 0.999999f);
+            return (uint32_t)(x * (float)(1u << bits));
+        };
+        auto spread = [](uint32_t v) {           // 5 bits -> every third bit
+            uint32_t r = 0;
+            for (int i = 0; i < 5; i++) r |= ((v >> i) & 1u) << (3 * i);
+            return r;
+        };
+#pragma omp parallel for schedule(dynamic, 1024) num_threads(nt)
+        for (int64_t k = 0; k < L; k++) {
+            std::vector<uint32_t> r;
+            g_rec = &r;
+            float closest = 1e30f;
+            int index = -1;
+            Counters c;
+            const RayData &rd = rays[idx[k]];
+            bvh_closest_hit(s, rd.origin, rd.dir, closest, index, c);
+            g_rec = nullptr;
+            rec[k].swap(r);
+            const V3 o = (rd.origin - s->min_coord) * s->inv_dimensions, d = 0.5f * (rd.dir + V3{1, 1, 1});
+            const uint32_t ko = spread(q(o.x, obits)) | spread(q(o.y, obits)) << 1 | spread(q(o.z, obits)) << 2;
+            const uint32_t kd = spread(q(d.x, dbits)) | spread(q(d.y, dbits)) << 1 | spread(q(d.z, dbits)) << 2;
+            fine[k] = ko << 15 | kd;
+        }
+        const uint64_t tri_base = (uint64_t)nn * 64;
+        for (int ord = 0; ord < 2; ord++) {
+            std::vector<int64_t> order(L);
+            for (int64_t k = 0; k < L; k++) order[k] = k;
+            if (ord == 1)
+                for (int64_t a = 0; a < L; a += tile) {
+                    const int64_t e = std::min<int64_t>(L, a + tile);
+                    std::stable_sort(order.begin() + a, order.begin() + e,
+                                     [&](int64_t x, int64_t y) { return fine[x] < fine[y]; });
+                }
+            // one model wave per eighth of the order (the queue shards), summed
+            double it = 0, itn = 0, itt = 0, lanes = 0, lines = 0, longest = 0;
+#pragma omp parallel for schedule(static, 1) num_threads(std::min(nt, 8)) reduction(+ : it, itn, itt, lanes, lines) \
+    reduction(max : longest)
+            for (int sh = 0; sh < 8; sh++) {
+                const int64_t lo = L * sh / 8, hi = L * (sh + 1) / 8;
+                int64_t next = lo;
+                int64_t ray[64];
+                size_t pos[64];
+                for (int l = 0; l < 64; l++) ray[l] = -1;
+                std::vector<uint64_t> ln;
+                while (true) {
+                    int idle = 0;
+                    for (int l = 0; l < 64; l++) idle += ray[l] < 0;
+                    if (idle >= refill || idle == 64)
+                        for (int l = 0; l < 64 && next < hi; l++)
+                            if (ray[l] < 0) {
+                                ray[l] = order[next++];
+                                pos[l] = 0;
+                                longest = std::max(longest, (double)rec[ray[l]].size());
+                            }
+                    bool any = false, anyn = false, anyt = false;
+                    ln.clear();
+                    for (int l = 0; l < 64; l++) {
+                        if (ray[l] < 0) continue;
+                        const auto &r = rec[ray[l]];
+                        if (pos[l] >= r.size()) { ray[l] = -1; continue; }
+                        const uint32_t x = r[pos[l]++];
+                        const bool tri = x & kRecTri;
+                        (tri ? anyt : anyn) = true;
+                        any = true;
+                        lanes += 1;
+                        const uint64_t a = tri ? tri_base + (uint64_t)(x & ~kRecTri) * 48 : (uint64_t)x * 64;
+                        ln.push_back(a / 128);
+                        if ((a + (tri ? 47 : 63)) / 128 != a / 128) ln.push_back((a + (tri ? 47 : 63)) / 128);
+                    }
+                    if (!any) {
+                        if (next >= hi) break;
+                        continue;
+                    }
+                    it += 1;
+                    itn += anyn;
+                    itt += anyt;
+                    std::sort(ln.begin(), ln.end());
+                    lines += (double)(std::unique(ln.begin(), ln.end()) - ln.begin());
+                }
+            }
+            out[ord * 6 + 0] = it;
+            out[ord * 6 + 1] = itn;
+            out[ord * 6 + 2] = itt;
+            out[ord * 6 + 3] = lanes;
+            out[ord * 6 + 4] = lines;
+            out[ord * 6 + 5] = longest;
+        }
+        return true;
+    };
+    const int64_t pixels = (int64_t)s->width * s->height;
+    std::vector<float> sum(pixels * 3);
+    Counters total;
+    uint64_t sorted = 0;
+    try {
+        gpu_pass(s, pass, sort != 0, sum.data(), total, nullptr, &sorted, threads);
+    } catch (...) {
+        g_bounce_hook = nullptr;
+        throw;
+    }
+    g_bounce_hook = nullptr;
+    if (!done) { g_err = "bounce not reached"; return -1; }
+    return 0;
+}
+
 int orc_render_pass_sums(const orc_scene *s, int sort, int pass_begin, int pass_count, float *out, int threads) {
     const int P = pass_total(s);
     if (pass_count < 0) pass_count = P - pass_begin;

@@ -95,6 +95,8 @@ int orc_pass_bounce_profile(const orc_scene *s, int sort, int pass, uint32_t *ma
 int orc_pass_chain_profile(const orc_scene *s, int sort, int pass, uint64_t *out, int threads);
 int orc_bounce_working_set(const orc_scene *s, int sort, int pass, int bounce, int window, int depth,
                            int windows_per_xcd, double *out, int threads);
+int orc_bounce_wave_model(const orc_scene *s, int sort, int pass, int bounce, int tile, int obits, int dbits,
+                          int refill, double *out, int threads);
 
 /* CPU-path semantics (raytracing.cu:122-163): bounce-invariant seed quirk, no keys,
  * no sort, sequential accumulate.  fb_out: W*H*3 (overwritten). pass_limit < 0 = all. */

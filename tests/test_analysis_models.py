@@ -39,3 +39,17 @@ def test_chain_profile_models_order():
     assert a[0, 4] > 0
     assert np.all(a[:, 4] >= a[:, 5]) and np.all(a[:, 5] >= a[:, 6]) and np.all(a[:, 7] >= a[:, 5])
     assert np.all(a[:, 0] >= a[:, 1])
+
+
+def test_wave_model_invariants():
+    """Re-ordering rays inside tiles changes which rays share a wave, never the work (tools/wave_model.py)."""
+    sc, L = _scene(), O.lib()
+    L.orc_bounce_wave_model.argtypes = [C.c_void_p] + [C.c_int] * 7 + [C.c_void_p, C.c_int]
+    out = np.zeros(12)
+    assert L.orc_bounce_wave_model(sc.h, 1, 0, 1, 256, 4, 2, 24, out.ctypes.data_as(C.c_void_p), 2) == 0
+    a, b = out[:6], out[6:]
+    assert a[3] > 0 and a[3] == b[3] and a[5] == b[5]               # same lane-steps, same longest ray
+    for o in (a, b):
+        assert o[0] > 0 and o[1] <= o[0] and o[2] <= o[0] and o[1] + o[2] >= o[0]
+        assert o[3] <= 64 * (o[1] + o[2])
+    assert L.orc_bounce_wave_model(sc.h, 1, 0, 1, 256, 4, 2, 0, out.ctypes.data_as(C.c_void_p), 2) != 0   # refill 0
