@@ -275,19 +275,24 @@ def roofline(excl, counted, launches, trace_ms, scene_bytes, spheres, workload, 
                                        "average trace dispatch duration (profiles/pmc_traffic.json "
                                        "trace_dur_ms_per_launch)"}
     iss = load_issue(workload)
-    timed = timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps)
+    # the timed regime's own PMC records (the driver's 20 concurrent passes) where they exist; one pass's otherwise
+    iss_t, pmc_t = load_issue(workload + TIMED_PMC), load_pmc(workload + TIMED_PMC)
+    if iss_t and steps >= 2:
+        timed = timed_regime(iss_t, pmc_t or pmc, counted, launches, scene_bytes, elapsed, steps, one_pass=iss)
+    else:
+        timed = timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps)
     if timed:
         roof = {"bound": "hbm", "achieved": timed["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": timed["frac"], "traffic": timed.get("measured_bytes_per_step"),
                 "traffic_frac": timed.get("measured_frac"), "regime": "timed step",
                 "kernel": kernel + ", inside the timed step",
                 "bytes_per_step": timed["algorithmic_bytes_per_step"], "kernel_ms_per_step": timed["ms_per_step"],
-                "traffic_unit": "bytes per step (the trace launches of one pass, rocprofv3 --pmc)",
+                "traffic_unit": "bytes per step (one pass's trace launches, rocprofv3 --pmc, %s)" % timed["regime"],
                 "achieved_def": "one pass's algorithmic trace bytes (24 B ray read per live segment past bounce 0 + "
                                 "8 B hit write per live segment + the scene once per XCD per launch) / the trace "
-                                "kernel's time per step (its SQ_WAVE_CYCLES share of one pass x ms_per_step, "
-                                "roofline.timed); traffic = the PMC fabric bytes of one pass's trace launches over "
-                                "the same time (traffic_frac)"}
+                                "kernel's time per step (its SQ_WAVE_CYCLES share of the timed regime's wave "
+                                "residency x ms_per_step, roofline.timed); traffic = the PMC fabric bytes of a "
+                                "pass's trace launches in that regime over the same time (traffic_frac)"}
     else:
         roof = {"bound": "hbm", "achieved": exclusive["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": exclusive["frac"], "traffic": traffic_ex, "traffic_frac": exclusive["traffic_frac"],
@@ -340,7 +345,10 @@ def roofline(excl, counted, launches, trace_ms, scene_bytes, spheres, workload, 
     return roof
 
 
-def timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps):
+TIMED_PMC = " | timed 20 passes"     # profiles/pmc_*.json key suffix: PMC runs of the driver's 20 concurrent passes
+
+
+def timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps, one_pass=None):
     """The dominant kernel inside the timed step (up to 20 passes sharing the chip): its time per step is
     taken as its share of one pass's wave residency (rocprofv3 --pmc SQ_WAVE_CYCLES of the trace launches
     over every kernel's, profiles/pmc_issue.json) times ms_per_step, so it never exceeds the step; over
@@ -356,8 +364,10 @@ def timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps):
     ms_pass = elapsed / steps * 1e3
     t = share * ms_pass / 1e3                       # s of trace per step
     alg = compulsory_trace_bytes(counted, scene_bytes, launches, per_xcd=True) / steps
+    concurrent = iss.get("passes_profiled", 1) > 1
     out = {"wave_cycle_share": round(share, 4), "ms_per_step": round(share * ms_pass, 4),
            "step_ms": round(ms_pass, 3),
+           "regime": ("the driver's %d concurrent passes" % iss["passes_profiled"]) if concurrent else "one pass alone",
            "algorithmic_bytes_per_step": int(alg), "achieved": round(alg / t / 1e9, 1),
            "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
     if pmc and pmc.get("trace_bytes_per_launch") and pmc.get("passes_profiled"):
@@ -367,12 +377,19 @@ def timed_regime(iss, pmc, counted, launches, scene_bytes, elapsed, steps):
     v_tr = iss.get("trace_per_pass", {}).get("SQ_INSTS_VALU")
     if v_tr:
         out["valu_frac"] = round(v_tr / t / 1e9 / VALU_PEAK_GWIS, 4)
-    out["def"] = ("trace_kernel within the timed step: its share of one pass's wave residency (SQ_WAVE_CYCLES of "
-                  "the trace launches / every kernel's, PMC run of one pass, profiles/pmc_issue.json: %s) x "
-                  "ms_per_step = its time per step (<= ms_per_step); frac = one pass's algorithmic trace bytes "
-                  "(as achieved_def) / that time / HBM peak; measured_frac = the PMC fabric bytes of the pass's "
-                  "trace launches (profiles/pmc_traffic.json) / that time / HBM peak; valu_frac = the pass's trace "
-                  "VALU wave-instructions / that time / the chip's VALU issue rate" % iss.get("run", ""))
+    if one_pass and one_pass.get("per_pass", {}).get("SQ_WAVE_CYCLES") and \
+            one_pass.get("trace_per_pass", {}).get("SQ_WAVE_CYCLES"):
+        s1 = one_pass["trace_per_pass"]["SQ_WAVE_CYCLES"] / one_pass["per_pass"]["SQ_WAVE_CYCLES"]
+        out["one_pass"] = {"wave_cycle_share": round(s1, 4), "ms_per_step": round(s1 * ms_pass, 4),
+                           "frac": round(alg / (s1 * ms_pass / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "def": "the same with the share of ONE pass profiled alone (profiles/pmc_issue.json: %s)"
+                                  % one_pass.get("run", "")}
+    out["def"] = ("trace_kernel within the timed step: its share of the wave residency (SQ_WAVE_CYCLES of the "
+                  "trace launches / every kernel's) in %s (profiles/pmc_issue.json: %s) x ms_per_step = its time "
+                  "per step (<= ms_per_step); frac = one pass's algorithmic trace bytes (as achieved_def) / that "
+                  "time / HBM peak; measured_frac = the PMC fabric bytes of a pass's trace launches in the same "
+                  "regime (profiles/pmc_traffic.json) / that time / HBM peak; valu_frac = a pass's trace VALU "
+                  "wave-instructions / that time / the chip's VALU issue rate" % (out["regime"], iss.get("run", "")))
     return out
 
 

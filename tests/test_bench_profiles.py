@@ -111,10 +111,16 @@ def test_roofline_headline_fits_the_step():
     assert abs(roof["frac"] * roof["peak"] * 1e9 * roof["kernel_ms_per_step"] / 1e3 - alg_step) / alg_step < 2e-3
     # at most the step's algorithmic bytes at the HBM peak over the whole step
     assert roof["frac"] * roof["peak"] * 1e9 * roof["kernel_ms_per_step"] / 1e3 <= alg_step * 1.002
-    pmc = bench.load_pmc(WORKLOAD)
+    # the timed regime's own PMC records (the driver's 20 concurrent passes) price it where they exist
+    pmc = bench.load_pmc(WORKLOAD + bench.TIMED_PMC) or bench.load_pmc(WORKLOAD)
     assert roof["traffic"] == t["measured_bytes_per_step"]
-    assert abs(roof["traffic_frac"] - pmc["trace_bytes_per_launch"] * pmc["trace_launches"] /
+    assert abs(roof["traffic_frac"] - pmc["trace_bytes_per_launch"] * pmc["trace_launches"] / pmc["passes_profiled"] /
                (roof["kernel_ms_per_step"] / 1e3) / 1e9 / 8000.0) < 2e-3
+    iss = bench.load_issue(WORKLOAD + bench.TIMED_PMC)
+    if iss:
+        assert t["regime"] == "the driver's 20 concurrent passes" and iss["passes_profiled"] == 20
+        assert t["wave_cycle_share"] == round(iss["trace_per_pass"]["SQ_WAVE_CYCLES"] / iss["per_pass"]["SQ_WAVE_CYCLES"], 4)
+        assert 0 < t["wave_cycle_share"] < t["one_pass"]["wave_cycle_share"] < 1
 
 
 def _final_lines():
