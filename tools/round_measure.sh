@@ -3,7 +3,8 @@
 # the first failure).  Outputs under gpurun_out/TAG/; copy what is judged into profiles/rNN/.
 #   part A: GPU test suite, smoke(), PMC passes of one profiled teapot pass (traffic -> summarised into
 #           profiles/pmc_traffic.json, which the bench reads for roofline.traffic; stall -> instruction
-#           counts in profiles/pmc_issue.json, read for roofline.valu; trace), the
+#           counts in profiles/pmc_issue.json, read for roofline.valu; the same two over the driver's 20
+#           concurrent passes, keyed "... | timed 20 passes", read for the roofline headline; trace), the
 #           headline bench line, the driver-style --steps 20 line, rocprofv3 kernel-trace summary.
 #   part B: bench lines of the other BASELINE configs, the strong-scaling probe, REPORT.pdf Table 1
 #           (their PMC records come from tools/pmc_configs.sh, run before part B).
@@ -33,6 +34,15 @@ if [ "$PART" = A ]; then
       --workload "teapot.scene 1920x1080 2048spp 16 bounces sort=on" \
       --run "rev $REV: python3 bench.py --steps 1 --warmup 0 --no-extras (tools/pmc.sh ${TAG}_st)" > $OUT/pmc_stall_teapot.txt || exit 1
   cp profiles/pmc_issue.json $OUT/pmc_issue.json
+  step pmc of the timed regime: the driver's 20 concurrent passes
+  W20="teapot.scene 1920x1080 2048spp 16 bounces sort=on | timed 20 passes"
+  bash tools/pmc.sh ${TAG}_t20st tools/pmc_groups/stall.txt --steps 20 > $OUT/pmc_t20st.log 2>&1 || { cat $OUT/pmc_t20st.log; exit 1; }
+  python3 tools/stall_summary.py ${TAG}_t20st --json profiles/pmc_issue.json --workload "$W20" \
+      --run "rev $REV: python3 bench.py --steps 20 --warmup 0 --no-extras (tools/pmc.sh ${TAG}_t20st)" > $OUT/pmc_stall_t20.txt || exit 1
+  bash tools/pmc.sh ${TAG}_t20tf tools/pmc_groups/traffic.txt --steps 20 > $OUT/pmc_t20tf.log 2>&1 || { cat $OUT/pmc_t20tf.log; exit 1; }
+  python3 tools/pmc_summary.py ${TAG}_t20tf --json profiles/pmc_traffic.json --workload "$W20" \
+      --run "rev $REV: python3 bench.py --steps 20 --warmup 0 --no-extras (tools/pmc.sh ${TAG}_t20tf)" > /dev/null || exit 1
+  cp profiles/pmc_issue.json profiles/pmc_traffic.json $OUT/
   bash tools/pmc.sh ${TAG}_tr tools/pmc_groups/trace.txt > $OUT/pmc_trc.log 2>&1 || { cat $OUT/pmc_trc.log; exit 1; }
   python3 tools/pmc_summary.py ${TAG}_tr > $OUT/pmc_trace_teapot.txt || exit 1
   step bench teapot
