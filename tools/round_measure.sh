@@ -34,7 +34,7 @@ if [ "$PART" = A ]; then
       --workload "teapot.scene 1920x1080 2048spp 16 bounces sort=on" \
       --run "rev $REV: python3 bench.py --steps 1 --warmup 0 --no-extras (tools/pmc.sh ${TAG}_st)" > $OUT/pmc_stall_teapot.txt || exit 1
   cp profiles/pmc_issue.json $OUT/pmc_issue.json
-  step pmc of the timed regime: the driver's 20 concurrent passes
+  step pmc of the timed regime, 20 concurrent passes
   W20="teapot.scene 1920x1080 2048spp 16 bounces sort=on | timed 20 passes"
   bash tools/pmc.sh ${TAG}_t20st tools/pmc_groups/stall.txt --steps 20 > $OUT/pmc_t20st.log 2>&1 || { cat $OUT/pmc_t20st.log; exit 1; }
   python3 tools/stall_summary.py ${TAG}_t20st --json profiles/pmc_issue.json --workload "$W20" \
