@@ -890,7 +890,7 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
 
 def frame_parity(fb, name, sort, image):
     """The timed region's whole frame (when it is the configured frame) hashed against the oracle's
-    (tests/golden/bench_frames.json: cornell, cornell_plus, spheres)."""
+    (tests/golden/bench_frames.json: cornell, cornell_plus, spheres, teapot in both sort modes)."""
     if fb is None or image is None:
         return {}
     try:

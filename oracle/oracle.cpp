@@ -873,14 +873,25 @@ void gpu_pass(const orc_scene *s, int p, bool sort, float *pass_sum, Counters &t
             for (int64_t k = 0; k < n; k++) h[orc_key_bucket(keys[k])]++;
         }
         if (sort && b + 1 != s->bounces) {              // raytracing.cu:238-247: stable sort pairs
-            std::vector<uint32_t> order(n);
-            for (int64_t k = 0; k < n; k++) order[k] = (uint32_t)k;
-            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t c) { return keys[a] < keys[c]; });
+            // cub::DeviceRadixSort::SortPairs is an LSD radix sort of the 32-bit keys: four stable 8-bit
+            // counting passes (a pass whose digit is the same for every key moves nothing and is skipped)
             idx2.resize(n);
             keys2.resize(n);
-            for (int64_t k = 0; k < n; k++) { idx2[k] = idx[order[k]]; keys2[k] = keys[order[k]]; }
-            idx.swap(idx2);
-            keys.swap(keys2);
+            for (int shift = 0; shift < 32; shift += 8) {
+                int64_t cnt[257] = {0};
+                for (int64_t k = 0; k < n; k++) cnt[((keys[k] >> shift) & 0xFF) + 1]++;
+                bool one = false;
+                for (int d = 0; d < 256; d++) one = one || cnt[d + 1] == n;
+                if (one) continue;
+                for (int d = 0; d < 256; d++) cnt[d + 1] += cnt[d];
+                for (int64_t k = 0; k < n; k++) {
+                    const int64_t to = cnt[(keys[k] >> shift) & 0xFF]++;
+                    keys2[to] = keys[k];
+                    idx2[to] = idx[k];
+                }
+                idx.swap(idx2);
+                keys.swap(keys2);
+            }
             *sorted += (uint64_t)n;
         }
     }

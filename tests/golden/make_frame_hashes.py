@@ -6,7 +6,8 @@ the BASELINE configs' full sizes, beyond bench_pass0.json's pass 0:
     512^2 x 256 spp x 8 (config 2), spheres 1024^2 x 1024 spp x 8 no_bvh (config 3);
   * the LAST (remainder) pass of teapot (config 4, 8 spp, generate seed remaining = 0) and lamp
     (config 5, 16 spp), sort on and off: pass 0 is already pinned, and the last pass is the one
-    whose rtc differs (raytracing.cu:224-225).
+    whose rtc differs (raytracing.cu:224-225);
+  * (round 6) the whole teapot frames, sort on and off (lamp's would take ~3.5 h each here).
 
 The GPU tests (tests/test_gpu_baseline_sizes.py) render the same frames / passes through the C ABI
 and compare hashes, so no oracle code runs on the GPU box for these sizes.  Reference loop:
@@ -39,6 +40,11 @@ JOBS = {
     "teapot last sort=off": ("teapot", False, "last"),
     "lamp last sort=on": ("lamp", True, "last"),
     "lamp last sort=off": ("lamp", False, "last"),
+    # round 6: the whole teapot frames too (~50 min each here); the lamp frames (~3.5 h each) are not generated
+    "teapot frame sort=on": ("teapot", True, "frame"),
+    "teapot frame sort=off": ("teapot", False, "frame"),
+    "lamp frame sort=on": ("lamp", True, "frame"),
+    "lamp frame sort=off": ("lamp", False, "frame"),
 }
 
 

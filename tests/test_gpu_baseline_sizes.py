@@ -6,7 +6,8 @@ SHA-256 fixtures the CPU oracle produced in the container:
     cornell_plus 512^2, spheres 1024^2 no_bvh, teapot 1080p x 16 and lamp 1080p x 32 bounces, both
     sort modes for teapot and lamp);
   * tests/golden/bench_frames.json (make_frame_hashes.py): the whole cornell, cornell_plus and
-    spheres frames, and the last (remainder) pass of teapot and lamp in both sort modes.
+    spheres frames, the last (remainder) pass of teapot and lamp in both sort modes, and (round 6) the
+    whole teapot frames in both sort modes.
 
 Reference loop: raytracing.cu:222-254 (pass rtc / remaining :224-229, process seeds :235, the
 reorder :238-247)."""
