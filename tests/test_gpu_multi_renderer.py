@@ -54,7 +54,7 @@ def test_multi_renderer_loopback(monkeypatch, world, scene, image, sort):
     try:
         assert m.ranks == world
         P = psc.passes
-        for n in (P, 3, -1):
+        for n in (P, 3, 1, 0, -1):         # 1 and 0: fewer passes than devices, an idle rank
             st = m.run(n)
             k = P if n < 0 else n
             ref, ost = osc.render(sort=sort, pass_begin=0, pass_count=k)
