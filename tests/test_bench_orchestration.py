@@ -1,4 +1,4 @@
-"""bench.py's own N-GPU orchestration, run end to end over gloo on CPU (world 2 and 4).
+"""bench.py's own N-GPU orchestration, run end to end over gloo on CPU (world 2, 4 and 8).
 
 bench.run() is the code the driver's SCALE run executes on every rank (torchrun, one process per
 GPU): the weak-scaling frame extension, the rank-0-only legs (exclusive pass, parity hash), the
@@ -126,7 +126,8 @@ def _worker(rank, world, port, tmp, steps):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,steps", [(2, None), (4, None), (2, 2), (4, 1)])
+# (8, 1): the driver's SCALE shape at N = 8 (one rank per GPU, weak-scaling frame extension)
+@pytest.mark.parametrize("world,steps", [(2, None), (4, None), (2, 2), (4, 1), (8, 1)])
 def test_bench_run_over_gloo(tmp_path, world, steps):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), steps), nprocs=world, join=True)
     recs = [json.load(open(tmp_path / ("rank%d.json" % r))) for r in range(world)]

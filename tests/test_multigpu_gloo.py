@@ -67,7 +67,7 @@ def _worker(rank, world, port, out_path, chunk, xrounds=None):
 
 
 @pytest.mark.parametrize("world,chunk,xrounds", [(2, 2, None), (3, None, None), (5, None, None),
-                                                 (2, None, 1), (3, 2, 1), (2, None, 2)])
+                                                 (2, None, 1), (3, 2, 1), (2, None, 2), (8, None, None)])
 def test_pass_sharded_frame_is_bitexact(tmp_path, world, chunk, xrounds):
     """xrounds: the overlapped exchange (an asynchronous renderer, slices exchanged every xrounds rounds)."""
     out = str(tmp_path / "fb.npy")
