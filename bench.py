@@ -846,6 +846,7 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
                 "passes_per_frame": P,
                 "n_ranks_seen": n_ranks_seen,
                 "hip_runtime": hip_runtimes(),
+                "passes_in_flight": passes_in_flight(inlib),
                 **({"frame_extended": "%d spp (%d passes) instead of %d, so that each of the %d GPUs renders its %d "
                                       "passes in one batch" % (frame_spp, P, spp, world, steps)}
                    if frame_spp != spp else {}),
@@ -886,6 +887,17 @@ def run(args, backend, cfg=None, json_out=None, golden=None):
             print(json.dumps(out), file=json_out, flush=True)
     ren.close()
     return {"line": out, "timed_fb": timed_fb, "my_passes": my_passes, "frame_passes": P} if rank == 0 else None
+
+
+def passes_in_flight(inlib):
+    """The passes a renderer keeps in flight (per GPU): 20, 16 inside rt_multi, at most RTAMD_INFLIGHT (bench.py sets
+    16 next to RCCL) and at most GPU_MAX_HW_QUEUES (rt_render.hip queues_granted)."""
+    cap = 16 if inlib else 20
+    e = os.environ.get("RTAMD_INFLIGHT")
+    if e and e.isdigit():
+        cap = min(cap, max(1, int(e)))
+    q = os.environ.get("GPU_MAX_HW_QUEUES", "")
+    return {"cap": min(cap, int(q) if q.isdigit() and int(q) > 0 else 4), "hw_queues": q or None}
 
 
 def frame_parity(fb, name, sort, image):

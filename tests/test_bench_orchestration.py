@@ -141,6 +141,7 @@ def test_bench_run_over_gloo(tmp_path, world, steps):
     assert all(r["log"] == [] for r in recs[1:])
     cfgd = line["config"]
     assert cfgd["n_ranks_seen"] == world and line["n_gpus"] == world
+    assert cfgd["passes_in_flight"]["cap"] == 16      # next to RCCL (bench.py's RTAMD_INFLIGHT)
     W, H, spp, bounces = CFG[1:5]
     if steps is None:
         frame_spp = spp
